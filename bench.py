@@ -1,0 +1,193 @@
+#!/usr/bin/env python3
+"""bench.py -- headline benchmark of the MI355X forward-warp hot path.
+
+Metric (BASELINE.json): Mpix/s forward-warped (768x1024, B=64) + %HBM roofline.
+One "step" = one FW pass (flow -> z-buffered splat -> resolve) over one batch
+of 64 synthetic 768x1024 images with C=6 channels per image ([RGB, depth,
+-flow], the preprocess.py:358/:386 call), inputs already resident in HBM.
+Half the images carry a disparity flow, half an ego-motion flow (per-image
+seeds 12345+i, camera parameters broadcast from rank 0 over RCCL).
+
+Multi-GPU: one process per GPU (torchrun), each rank warps its own 64-image
+shard (weak scaling, no data-path collective); timing is barrier-bracketed and
+the max over ranks is taken.  Rank 0 prints ONE JSON line.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "Mpix/s forward-warped (768×1024, B=64) + %HBM roofline, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=64, help="images per GPU")
+    ap.add_argument("--height", type=int, default=768)
+    ap.add_argument("--width", type=int, default=1024)
+    ap.add_argument("--ego-fraction", type=float, default=0.5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline wall budget")
+    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
+    ap.add_argument("--check", action="store_true", help="verify one image against the oracle")
+    return ap.parse_args()
+
+
+def cpu_baseline(obj, flow, depth, budget_s, threads):
+    """Oracle (C restatement of fw_cuda_kernel.cu:28-47 + fw.py:27-43, OpenMP
+    over (image, channel) planes like the reference's <<<B, C>>> grid), timed
+    on this box's host cores over a bounded sample of the same workload."""
+    from oracle import oracle  # test infrastructure: baseline leg only
+    n_img = min(8, obj.shape[0])
+    half = n_img // 2
+    B = obj.shape[0]
+    idx = list(range(half)) + list(range(B - (n_img - half), B))  # both flow kinds
+    o = obj[idx].cpu().numpy()
+    f = flow[idx].cpu().numpy()
+    d = depth[idx].cpu().numpy()
+    if threads <= 0:
+        threads = min(16, os.cpu_count() or 1)
+    oracle.fw_flow(o[:1], f[:1], d[:1], nthreads=threads)  # warm (build + page-in)
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        oracle.fw_flow(o, f, d, nthreads=threads)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    px = reps * n_img * o.shape[2] * o.shape[3]
+    return {"value": px / el / 1e6, "unit": "Mpix/s", "cores": threads, "kind": "port",
+            "sample": f"{n_img} images (of the {B}-image batch, both flow kinds) x {reps} reps, "
+                      f"C={o.shape[1]}, {o.shape[2]}x{o.shape[3]}, oracle/fw_oracle.c serial-per-plane "
+                      f"loop, {el:.1f} s wall on {platform.processor() or platform.machine()}"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    from opticalflowfromdepth_amd import forward_warp_flow, shard, synth
+    from opticalflowfromdepth_amd import _native
+
+    B, H, W = args.batch, args.height, args.width
+    n_total = B * world
+    seeds = [shard.image_seed(i) for i in range(n_total)]
+    s_all, T_all = shard.broadcast_camera_params(seeds, device=dev)     # RCCL broadcast (setup)
+    a, b = shard.shard_range(n_total, world, rank)
+    obj, flow, depth = synth.stage_one_batch(seeds[a:b], H, W, dev, ego_fraction=args.ego_fraction,
+                                             camera=(s_all[a:b], T_all[a:b]))
+    C = obj.shape[1]
+    out = (torch.empty_like(obj), torch.empty_like(depth), torch.empty_like(depth))
+    _native.lib()
+    torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        forward_warp_flow(obj, flow, depth, out=out)
+    torch.cuda.synchronize()
+
+    if args.check and rank == 0:
+        from oracle import oracle
+        exp = oracle.fw_flow(obj[:1].cpu().numpy(), flow[:1].cpu().numpy(), depth[:1].cpu().numpy())
+        ok = all((g[:1].cpu().numpy() == e).all() for g, e in zip(out, exp))
+        print(f"# check vs oracle (image 0): {'OK' if ok else 'MISMATCH'}", file=sys.stderr)
+
+    stream = torch.cuda.current_stream(dev)
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        starts[k].record(stream)
+        forward_warp_flow(obj, flow, depth, out=out)
+        ends[k].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    ev_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
+    dev_ms = sum(ev_ms) / len(ev_ms)
+
+    t = torch.tensor([wall, dev_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall, dev_ms_max = float(t[0]), float(t[1])
+
+    px_step_rank = B * H * W
+    bytes_per_px = (2 * C + 5) * 4  # algorithmic: obj C + flow 2 + depth in; out C + valid + coll
+    value = n_total * H * W * args.steps / wall / 1e6
+    achieved_gbs = px_step_rank * bytes_per_px / (dev_ms / 1e3) / 1e9
+
+    traffic = None
+    traffic_note = None
+    pmc_file = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc_file):
+        try:
+            pm = json.load(open(pmc_file))
+            if pm.get("config") == [B, C, H, W]:
+                traffic = pm.get("hbm_bytes_per_step")
+                traffic_note = pm.get("source")
+        except Exception:
+            pass
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(obj, flow, depth, args.cpu_seconds, args.cpu_threads)
+
+    if rank == 0:
+        rec = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "Mpix/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(wall / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded depth fields -> normalize_depth -> disparity / ego-motion flow)",
+            "config": {"workload": f"FW forward warp, {H}x{W}, B={B} per GPU, C={C} "
+                                   f"(BASELINE config 3/4)", "global_batch": n_total, "height": H,
+                       "width": W, "channels": C, "ego_fraction": args.ego_fraction,
+                       "parallelism": f"shard{world} (images, no data-path collective)"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
+                         "traffic": traffic,
+                         "kernel": "ofd_fw forward_warp_flow (splat + resolve launches of one call)",
+                         "algorithmic_bytes_per_px": bytes_per_px,
+                         "event_ms_per_call": round(dev_ms, 4),
+                         "traffic_source": traffic_note},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,105 @@
+/*
+ * ofd_fw.h -- C ABI of the MI355X forward-warp (z-buffered splat) engine.
+ *
+ * Plain pointers and sizes only; every device pointer is a gfx950 device
+ * allocation, every entry point is asynchronous on the given HIP stream
+ * (`stream` is a hipStream_t passed as void*, NULL = the legacy default
+ * stream).  All tensors are dense, contiguous, NCHW.
+ *
+ * Entry point -> reference interface it replaces (paths in the reference
+ * checkout AegeanKI/OpticalFlowFromDepth @ 2024_08_07):
+ *
+ *   ofd_fw_forward_warping_f32 / _f64
+ *       fw_cuda.forward_warping(obj, safe_y, safe_x, depth)
+ *       -- alt_cuda/fw_cuda.cpp:15-26 (binding), alt_cuda/fw_cuda_kernel.cu:52-83
+ *          (host: allocate + launch) and :9-49 (kernel).  Same semantics, any B.
+ *   ofd_fw_forward_warp_flow_f32 / _f64flow
+ *       alt_cuda.fw.FW.forward(obj, flow, depth)  -- alt_cuda/fw.py:19-59,
+ *       batched: the meshgrid add / clamp / int64 truncation of fw.py:27-42 is
+ *       done inside the kernel, the add in the flow's dtype (fw.py:31).
+ *   ofd_fw_workspace_bytes / ofd_fw_workspace_init
+ *       no reference counterpart: the reference allocates its z-buffer `dlut`
+ *       per call (fw_cuda_kernel.cu:58); here the caller owns a reusable
+ *       key workspace that every call leaves in its initial state.
+ *
+ * Semantics (identical to the serial loop fw_cuda_kernel.cu:28-47):
+ *   per target pixel t of image b:
+ *     winner(t)    = the source s with the smallest float depth among sources
+ *                    landing on t with depth < 1000; ties -> smallest raster
+ *                    index s = j*W + i.  (-0.0 == +0.0; NaN never wins.)
+ *     output[b,c,t]= obj[b,c,winner] or 0 if no winner
+ *     valid[b,0,t] = 1 if any source landed on t, else 0
+ *     collision[b,0,t] = 1 if valid and no winner, else 0
+ *   Defined where the reference is undefined: a source whose coordinate is
+ *   NaN or truncates outside [0,W)x[0,H) is dropped.
+ *
+ * Return codes: 0 = success; <0 = OFD_FW_E* below; >0 = a hipError_t from the
+ * launch.  ofd_fw_strerror() names any of them.
+ */
+#ifndef OFD_FW_H
+#define OFD_FW_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OFD_FW_ABI_VERSION 1
+
+enum {
+    OFD_FW_OK = 0,
+    OFD_FW_EINVAL = -1,      /* null pointer or negative/zero-sized dimension mismatch */
+    OFD_FW_ETOOBIG = -2,     /* H*W >= 2^31 (source index must fit 31 bits) */
+    OFD_FW_EWORKSPACE = -3,  /* workspace null or smaller than ofd_fw_workspace_bytes() */
+    OFD_FW_EALIGN = -4       /* a pointer is not 4-byte (f32) / 8-byte (f64, workspace) aligned */
+};
+
+/* ABI version of the loaded library (OFD_FW_ABI_VERSION at build time). */
+int ofd_fw_abi_version(void);
+
+/* Human-readable name of a return code (static storage). */
+const char *ofd_fw_strerror(int code);
+
+/* Bytes of key workspace a call with these sizes needs.  f64 != 0 for the
+ * float64 op.  The workspace is reused across calls and must be initialised
+ * once with ofd_fw_workspace_init(); every successful call leaves it
+ * initialised again. */
+size_t ofd_fw_workspace_bytes(int64_t B, int64_t H, int64_t W, int f64);
+
+/* Put `bytes` of workspace into its initial state (async on `stream`). */
+int ofd_fw_workspace_init(void *workspace, size_t bytes, void *stream);
+
+/* fw_cuda.forward_warping, float32.  obj/output [B,C,H,W]; safe_y, safe_x,
+ * depth, valid, collision [B,1,H,W].  Coordinates are truncated toward zero. */
+int ofd_fw_forward_warping_f32(const float *obj, const float *safe_y, const float *safe_x,
+                               const float *depth, float *output, float *valid,
+                               float *collision, int64_t B, int64_t C, int64_t H, int64_t W,
+                               void *workspace, size_t workspace_bytes, void *stream);
+
+/* fw_cuda.forward_warping, float64 (AT_DISPATCH_FLOATING_TYPES double path). */
+int ofd_fw_forward_warping_f64(const double *obj, const double *safe_y, const double *safe_x,
+                               const double *depth, double *output, double *valid,
+                               double *collision, int64_t B, int64_t C, int64_t H, int64_t W,
+                               void *workspace, size_t workspace_bytes, void *stream);
+
+/* FW.forward, batched.  obj [B,C,H,W] f32, flow [B,2,H,W] (ch0 = x, ch1 = y)
+ * f32, depth [B,1,H,W] f32 -> output [B,C,H,W], valid, collision [B,1,H,W]. */
+int ofd_fw_forward_warp_flow_f32(const float *obj, const float *flow, const float *depth,
+                                 float *output, float *valid, float *collision,
+                                 int64_t B, int64_t C, int64_t H, int64_t W,
+                                 void *workspace, size_t workspace_bytes, void *stream);
+
+/* FW.forward with a float64 flow: p0 + flow is evaluated in float64 exactly
+ * as fw.py:31 promotes it; everything else float32. */
+int ofd_fw_forward_warp_flow_f64flow(const float *obj, const double *flow, const float *depth,
+                                     float *output, float *valid, float *collision,
+                                     int64_t B, int64_t C, int64_t H, int64_t W,
+                                     void *workspace, size_t workspace_bytes, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* OFD_FW_H */

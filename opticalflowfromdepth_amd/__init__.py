@@ -1,0 +1,15 @@
+"""opticalflowfromdepth_amd -- MI355X-native forward-warp (z-buffered splat) engine.
+
+The hot path of AegeanKI/OpticalFlowFromDepth (alt_cuda/fw_cuda_kernel.cu,
+alt_cuda/fw_cuda.cpp, alt_cuda/fw.py) rebuilt as hand-written HIP kernels for
+gfx950 behind a C ABI (include/ofd_fw.h), with the reference's Python surface:
+
+* ``FW``               -- drop-in for ``alt_cuda.fw.FW``
+* ``forward_warping``  -- drop-in for the extension op ``fw_cuda.forward_warping``
+* ``forward_warp_flow``-- batched FW core (flow -> splat in one native call)
+"""
+from .fw import FW
+from .ops import forward_warp_flow, forward_warping
+
+__all__ = ["FW", "forward_warping", "forward_warp_flow"]
+__version__ = "0.1.0"

@@ -1,0 +1,86 @@
+"""Loader for the native forward-warp library (libofd_fw.so, C ABI in include/ofd_fw.h).
+
+The library is built in-tree by :func:`opticalflowfromdepth_amd.build.build_native`
+(hipcc --offload-arch=gfx950).  There is deliberately NO fallback: if the
+library is missing or does not load, every op raises -- a silent CPU or eager
+torch path would hide that the HIP kernels are not the thing running.
+
+torch is imported first so that its HIP runtime (libamdhip64.so.7, shipped in
+torch/lib) is the one the library binds to: stream handles from
+``torch.cuda.current_stream()`` are then valid inside the library.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  -- must precede the CDLL load (shared HIP runtime)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_build", "libofd_fw.so")
+ABI_VERSION = 1
+
+_lock = threading.Lock()
+_lib = None
+
+# (name, argtypes, restype) for every symbol declared in include/ofd_fw.h
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_SZ = ctypes.c_size_t
+SIGNATURES = {
+    "ofd_fw_abi_version": ([], ctypes.c_int),
+    "ofd_fw_strerror": ([ctypes.c_int], ctypes.c_char_p),
+    "ofd_fw_workspace_bytes": ([_I64, _I64, _I64, ctypes.c_int], _SZ),
+    "ofd_fw_workspace_init": ([_P, _SZ, _P], ctypes.c_int),
+    "ofd_fw_forward_warping_f32": ([_P] * 7 + [_I64] * 4 + [_P, _SZ, _P], ctypes.c_int),
+    "ofd_fw_forward_warping_f64": ([_P] * 7 + [_I64] * 4 + [_P, _SZ, _P], ctypes.c_int),
+    "ofd_fw_forward_warp_flow_f32": ([_P] * 6 + [_I64] * 4 + [_P, _SZ, _P], ctypes.c_int),
+    "ofd_fw_forward_warp_flow_f64flow": ([_P] * 6 + [_I64] * 4 + [_P, _SZ, _P], ctypes.c_int),
+}
+
+
+class NativeLibraryError(RuntimeError):
+    """The HIP forward-warp library is missing or unusable."""
+
+
+def _try_build():
+    # Build in place when the source tree is present and hipcc is available
+    # (e.g. a fresh checkout); otherwise report what is missing.
+    from . import build as _build
+    _build.build_native()
+
+
+def lib():
+    """Return the loaded ctypes library, building it once if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            try:
+                _try_build()
+            except Exception as e:  # pragma: no cover - depends on toolchain
+                raise NativeLibraryError(
+                    f"libofd_fw.so not found at {LIB_PATH} and building it failed: {e}") from e
+        try:
+            l = ctypes.CDLL(LIB_PATH)
+        except OSError as e:
+            raise NativeLibraryError(f"cannot load {LIB_PATH}: {e}") from e
+        for name, (argt, rest) in SIGNATURES.items():
+            fn = getattr(l, name)
+            fn.argtypes = argt
+            fn.restype = rest
+        v = l.ofd_fw_abi_version()
+        if v != ABI_VERSION:
+            raise NativeLibraryError(f"libofd_fw ABI {v}, python expects {ABI_VERSION}; rebuild")
+        _lib = l
+        return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().ofd_fw_strerror(rc).decode()
+        raise RuntimeError(f"{what} failed: {msg} (code {rc})")

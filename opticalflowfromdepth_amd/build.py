@@ -1,0 +1,52 @@
+"""In-tree build of the native forward-warp library for gfx950.
+
+``python -m opticalflowfromdepth_amd.build`` or ``build_native()`` compiles
+csrc/ofd_fw.hip with hipcc into ``_build/libofd_fw.so`` (C ABI, include/ofd_fw.h).
+The .so is git-ignored but travels with the repo snapshot to the GPU box.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(_HERE)
+SRC = os.path.join(_HERE, "csrc", "ofd_fw.hip")
+HDR = os.path.join(REPO, "include", "ofd_fw.h")
+OUT_DIR = os.path.join(_HERE, "_build")
+OUT = os.path.join(OUT_DIR, "libofd_fw.so")
+ARCH = os.environ.get("OFD_OFFLOAD_ARCH", "gfx950")
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise FileNotFoundError("hipcc not found (set HIPCC or install ROCm)")
+
+
+def needs_build() -> bool:
+    if not os.path.exists(OUT):
+        return True
+    t = os.path.getmtime(OUT)
+    return any(os.path.getmtime(p) > t for p in (SRC, HDR))
+
+
+def build_native(force: bool = False, verbose: bool = False) -> str:
+    if not force and not needs_build():
+        return OUT
+    os.makedirs(OUT_DIR, exist_ok=True)
+    tmp = OUT + f".tmp{os.getpid()}"
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-Wall", "-I", os.path.join(REPO, "include"), "-o", tmp, SRC]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, OUT)  # atomic: concurrent builders never expose a half-written .so
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build_native(force="--force" in sys.argv, verbose=True))

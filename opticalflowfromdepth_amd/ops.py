@@ -1,0 +1,149 @@
+"""Torch-facing forward-warp ops over the C ABI (include/ofd_fw.h).
+
+``forward_warping`` mirrors the reference extension op
+``fw_cuda.forward_warping(obj, safe_y, safe_x, depth) -> [output, valid, collision]``
+(alt_cuda/fw_cuda.cpp:15-30, alt_cuda/fw_cuda_kernel.cu:52-83): same argument
+meaning, same checks and messages, same outputs, for any batch size B.
+
+``forward_warp_flow`` is the batched FW.forward path (alt_cuda/fw.py:19-59)
+with the coordinate arithmetic fused into the splat kernel.
+
+Both launch asynchronously on the current HIP stream of the input's device.
+There is no CPU path: the reference raises for non-GPU tensors
+(fw_cuda.cpp:11) and so does this module.
+"""
+from __future__ import annotations
+
+import threading
+from typing import Dict, List, Tuple
+
+import torch
+
+from . import _native
+
+_F32, _F64 = torch.float32, torch.float64
+
+# Reusable key workspaces, one per (device, stream); each call leaves its
+# workspace in the initial all-ones state (see include/ofd_fw.h).
+_ws_lock = threading.Lock()
+_workspaces: Dict[Tuple[int, int], torch.Tensor] = {}
+
+
+def _check_input(x: torch.Tensor, name: str) -> None:
+    # fw_cuda.cpp:11-13 (CHECK_CUDA / CHECK_CONTIGUOUS)
+    if not isinstance(x, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor")
+    if not x.is_cuda:
+        raise RuntimeError(f"{name} must be a CUDA tensor")
+    if not x.is_contiguous():
+        raise RuntimeError(f"{name} must be contiguous")
+
+
+def workspace(device: torch.device, nbytes: int, stream: torch.cuda.Stream) -> torch.Tensor:
+    """A >= nbytes initialised key workspace for (device, stream)."""
+    key = (device.index, stream.cuda_stream)
+    with _ws_lock:
+        ws = _workspaces.get(key)
+        if ws is None or ws.numel() < nbytes:
+            with torch.cuda.device(device), torch.cuda.stream(stream):
+                ws = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=device)
+            _native.check(_native.lib().ofd_fw_workspace_init(ws.data_ptr(), ws.numel(), stream.cuda_stream),
+                          "ofd_fw_workspace_init")
+            _workspaces[key] = ws
+        return ws
+
+
+def _ws_bytes(B: int, H: int, W: int, f64: bool) -> int:
+    return int(_native.lib().ofd_fw_workspace_bytes(B, H, W, 1 if f64 else 0))
+
+
+def forward_warping(obj: torch.Tensor, safe_y: torch.Tensor, safe_x: torch.Tensor,
+                    depth: torch.Tensor) -> List[torch.Tensor]:
+    """Drop-in for ``fw_cuda.forward_warping`` (alt_cuda/fw_cuda.cpp:15-26).
+
+    obj [B,C,H,W]; safe_y, safe_x, depth [B,1,H,W]; one float dtype (float32 or
+    float64) for all four.  Coordinates are truncated toward zero as the
+    reference's accessor indexing does.  Returns ``[output, valid, collision]``
+    with output [B,C,H,W] and valid/collision [B,1,H,W] in that dtype.
+    """
+    for x, n in ((obj, "obj"), (safe_y, "safe_y"), (safe_x, "safe_x"), (depth, "depth")):
+        _check_input(x, n)
+    if obj.dim() != 4:
+        raise RuntimeError(f"obj must be 4-D [B,C,H,W], got {obj.dim()}-D")
+    B, C, H, W = obj.shape
+    for x, n in ((safe_y, "safe_y"), (safe_x, "safe_x"), (depth, "depth")):
+        if tuple(x.shape) != (B, 1, H, W):
+            raise RuntimeError(f"{n} must have shape {(B, 1, H, W)}, got {tuple(x.shape)}")
+        if x.dtype != obj.dtype:
+            raise RuntimeError(f"expected scalar type {obj.dtype} for {n} but found {x.dtype}")
+        if x.device != obj.device:
+            raise RuntimeError(f"{n} is on {x.device}, obj on {obj.device}")
+    if obj.dtype not in (_F32, _F64):
+        raise RuntimeError(f"forward_warping supports float32/float64, got {obj.dtype}")
+    f64 = obj.dtype == _F64
+    dev = obj.device
+    with torch.cuda.device(dev):  # fw_cuda.cpp:24 device guard
+        stream = torch.cuda.current_stream(dev)
+        output = torch.empty_like(obj)
+        valid = torch.empty_like(depth)
+        collision = torch.empty_like(depth)
+        nbytes = _ws_bytes(B, H, W, f64)
+        ws = workspace(dev, nbytes, stream) if nbytes else None
+        fn = _native.lib().ofd_fw_forward_warping_f64 if f64 else _native.lib().ofd_fw_forward_warping_f32
+        rc = fn(obj.data_ptr(), safe_y.data_ptr(), safe_x.data_ptr(), depth.data_ptr(),
+                output.data_ptr(), valid.data_ptr(), collision.data_ptr(), B, C, H, W,
+                ws.data_ptr() if ws is not None else None, ws.numel() if ws is not None else 0,
+                stream.cuda_stream)
+        _native.check(rc, "forward_warping")
+    return [output, valid, collision]
+
+
+def forward_warp_flow(obj: torch.Tensor, flow: torch.Tensor, depth: torch.Tensor,
+                      out: Tuple[torch.Tensor, torch.Tensor, torch.Tensor] = None
+                      ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """Batched FW.forward core (alt_cuda/fw.py:27-54) in one native call.
+
+    obj [B,C,H,W] float32, flow [B,2,H,W] float32 or float64 (channel 0 = x /
+    u, channel 1 = y / v), depth [B,1,H,W] float32, all contiguous on one
+    device.  Target = trunc(clamp(p0 + flow)) with the add in the flow's dtype.
+    ``out`` optionally supplies preallocated (output, valid, collision).
+    """
+    for x, n in ((obj, "obj"), (flow, "flow"), (depth, "depth")):
+        _check_input(x, n)
+    if obj.dim() != 4:
+        raise RuntimeError(f"obj must be 4-D [B,C,H,W], got {obj.dim()}-D")
+    B, C, H, W = obj.shape
+    if tuple(flow.shape) != (B, 2, H, W):
+        raise RuntimeError(f"flow must have shape {(B, 2, H, W)}, got {tuple(flow.shape)}")
+    if tuple(depth.shape) != (B, 1, H, W):
+        raise RuntimeError(f"depth must have shape {(B, 1, H, W)}, got {tuple(depth.shape)}")
+    if obj.dtype != _F32 or depth.dtype != _F32:
+        raise RuntimeError("forward_warp_flow expects float32 obj and depth")
+    if flow.dtype not in (_F32, _F64):
+        raise RuntimeError(f"flow must be float32 or float64, got {flow.dtype}")
+    if flow.device != obj.device or depth.device != obj.device:
+        raise RuntimeError("obj, flow and depth must be on one device")
+    dev = obj.device
+    with torch.cuda.device(dev):
+        stream = torch.cuda.current_stream(dev)
+        if out is None:
+            output = torch.empty_like(obj)
+            valid = torch.empty_like(depth)
+            collision = torch.empty_like(depth)
+        else:
+            output, valid, collision = out
+            for x, n, shp in ((output, "output", (B, C, H, W)), (valid, "valid", (B, 1, H, W)),
+                              (collision, "collision", (B, 1, H, W))):
+                _check_input(x, n)
+                if tuple(x.shape) != shp or x.dtype != _F32 or x.device != dev:
+                    raise RuntimeError(f"out {n} must be float32 {shp} on {dev}")
+        nbytes = _ws_bytes(B, H, W, False)
+        ws = workspace(dev, nbytes, stream) if nbytes else None
+        lib = _native.lib()
+        fn = lib.ofd_fw_forward_warp_flow_f64flow if flow.dtype == _F64 else lib.ofd_fw_forward_warp_flow_f32
+        rc = fn(obj.data_ptr(), flow.data_ptr(), depth.data_ptr(), output.data_ptr(), valid.data_ptr(),
+                collision.data_ptr(), B, C, H, W,
+                ws.data_ptr() if ws is not None else None, ws.numel() if ws is not None else 0,
+                stream.cuda_stream)
+        _native.check(rc, "forward_warp_flow")
+    return output, valid, collision

@@ -1,0 +1,259 @@
+"""tests/golden/make_golden.py -- generates the committed golden fixtures.
+
+Run in the BUILD container only (it reads /root/reference, which does not exist
+on the GPU box):
+
+    python tests/golden/make_golden.py
+
+What it does, and what each fixture pins:
+
+* ``fw_wrapper.npz`` -- the reference's own ``alt_cuda/fw.py`` (imported from
+  /root/reference, unmodified) driven with 3-D inputs exactly as preprocess.py
+  calls it, with ``fw_cuda`` provided by the CPU oracle (oracle/fw_oracle.c,
+  the literal restatement of fw_cuda_kernel.cu:28-47).  Pins the wrapper
+  arithmetic (meshgrid, add in the flow's dtype, clamp, int64 truncation,
+  casts: fw.py:27-43) with the reference's own code.
+* ``fw_op.npz`` -- op-level ``forward_warping(obj, safe_y, safe_x, depth)`` cases
+  (B up to 3, C in {1,2,4,6,7}, ties, depth >= 1000, -0.0, negative depths,
+  hot spots, float64), expected outputs from the oracle loop, cross-checked
+  here against the independent lexmin formulation before being written.
+* ``pipeline.npz`` -- synthetic depth maps pushed through the reference's own
+  ``utils.normalize_depth`` / ``fix_warped_depth`` / ``get_random`` /
+  ``set_seed`` (function bodies taken from /root/reference/utils.py by AST,
+  so cv2 is not needed), ``Plausible``/``Convert`` (verbatim text slice
+  preprocess.py:184-298 -- the file as a whole does not parse, SyntaxError at
+  :463) and ``geometry.py`` (imported as is): disparity and ego-motion flows
+  with fixed seeds, and FW outputs on them.  Pins
+  opticalflowfromdepth_amd.synth (flows within 1e-5) and realistic FW cases.
+
+Nothing from /root/reference is copied into the repo: only numeric arrays.
+"""
+from __future__ import annotations
+
+import ast
+import importlib.util
+import math
+import os
+import random
+import sys
+import types
+
+import numpy as np
+import torch
+
+REF = os.environ.get("OFD_REFERENCE", "/root/reference")
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+
+from oracle import oracle  # noqa: E402  (test infrastructure)
+
+
+# ---------------------------------------------------------------- reference loaders
+def _oracle_fw_cuda_module():
+    """A module object named fw_cuda whose forward_warping is the CPU oracle."""
+    m = types.ModuleType("fw_cuda")
+
+    def forward_warping(obj, safe_y, safe_x, depth):
+        out, valid, coll = oracle.forward_warping(
+            obj.numpy(), safe_y.numpy(), safe_x.numpy(), depth.numpy())
+        return [torch.from_numpy(out), torch.from_numpy(valid), torch.from_numpy(coll)]
+
+    m.forward_warping = forward_warping
+    return m
+
+
+def load_reference_fw():
+    sys.modules["fw_cuda"] = _oracle_fw_cuda_module()
+    spec = importlib.util.spec_from_file_location("ref_alt_cuda_fw", os.path.join(REF, "alt_cuda", "fw.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def load_reference_geometry():
+    spec = importlib.util.spec_from_file_location("geometry", os.path.join(REF, "geometry.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    sys.modules["geometry"] = mod
+    return mod
+
+
+def load_reference_utils_subset():
+    """utils.py functions needed on the path, taken by AST (cv2 is absent here)."""
+    src = open(os.path.join(REF, "utils.py")).read()
+    tree = ast.parse(src)
+    want = {"get_random", "normalize_depth", "fix_warped_depth", "set_seed", "smooth_closer"}
+    body = [n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name in want]
+    mod = types.ModuleType("utils")
+    mod.__dict__.update(torch=torch, np=np, random=random, math=math)
+    exec(compile(ast.Module(body=body, type_ignores=[]), os.path.join(REF, "utils.py"), "exec"), mod.__dict__)
+    return mod
+
+
+def load_reference_plausible_convert(utils_mod, geometry_mod):
+    """Verbatim text slice preprocess.py:184-298 (class Plausible, class Convert)."""
+    lines = open(os.path.join(REF, "preprocess.py")).read().split("\n")
+    text = "\n".join(lines[183:298])
+    assert text.startswith("class Plausible"), text[:40]
+    ns = dict(torch=torch, math=math, utils=utils_mod, geometry=geometry_mod)
+    exec(compile(text, os.path.join(REF, "preprocess.py"), "exec"), ns)
+    return ns["Plausible"], ns["Convert"]
+
+
+# ---------------------------------------------------------------- synthetic inputs
+def synth_depth(h, w, seed):
+    """Smooth synthetic raw depth (opticalflowfromdepth_amd.synth.synthetic_depth_np)."""
+    from opticalflowfromdepth_amd.synth import synthetic_depth_np
+    return synthetic_depth_np(h, w, seed)
+
+
+def synth_rgb(h, w, seed):
+    rng = np.random.default_rng(seed + 1000)
+    return np.floor(rng.uniform(0, 256, (3, h, w))).astype(np.float32)
+
+
+# ---------------------------------------------------------------- fixtures
+def make_op_cases():
+    rng = np.random.default_rng(1234)
+    cases = {}
+    specs = [
+        # (name, B, C, H, W, dtype, kind)
+        ("ties_c1", 2, 1, 17, 23, np.float32, "ties"),
+        ("ties_c2", 1, 2, 24, 32, np.float32, "ties"),
+        ("ties_c4", 3, 4, 16, 20, np.float32, "ties"),
+        ("ties_c6", 2, 6, 24, 32, np.float32, "ties"),
+        ("ties_c7", 1, 7, 31, 29, np.float32, "ties"),
+        ("coll_c6", 2, 6, 20, 24, np.float32, "collide"),
+        ("negzero_c3", 1, 3, 16, 16, np.float32, "negzero"),
+        ("hotspot_c6", 1, 6, 32, 48, np.float32, "hotspot"),
+        ("nonint_c2", 2, 2, 18, 22, np.float32, "nonint"),
+        ("ties_f64_c4", 2, 4, 20, 24, np.float64, "ties"),
+        ("ragged_1x1", 1, 3, 1, 1, np.float32, "ties"),
+        ("ragged_1xw", 1, 2, 1, 37, np.float32, "ties"),
+        ("ragged_hx1", 2, 2, 41, 1, np.float32, "ties"),
+    ]
+    for name, B, C, H, W, dt, kind in specs:
+        obj = rng.standard_normal((B, C, H, W)).astype(dt)
+        flow = (rng.standard_normal((B, 2, H, W)) * 4).astype(np.float32)
+        depth = rng.integers(1, 4, (B, 1, H, W)).astype(dt)
+        if kind == "collide":
+            depth[rng.random(depth.shape) < 0.3] = 1000.0
+            depth[rng.random(depth.shape) < 0.2] = 5000.0
+        if kind == "negzero":
+            depth = rng.choice(np.array([0.0, -0.0, -1.0, 2.0], dt), size=(B, 1, H, W))
+        if kind == "hotspot":
+            flow = (rng.standard_normal((B, 2, H, W)) * 200).astype(np.float32)
+        sy, sx = oracle.safe_coords(flow)
+        if kind == "nonint":  # raw, non-integer in-range coordinates (truncated by the op)
+            sx = rng.uniform(-0.99, W - 0.01, (B, 1, H, W)).astype(np.float32)
+            sy = rng.uniform(-0.99, H - 0.01, (B, 1, H, W)).astype(np.float32)
+        sy, sx = sy.astype(dt), sx.astype(dt)
+        out, valid, coll = oracle.forward_warping(obj, sy, sx, depth)
+        if dt == np.float32:
+            lo, lv, lc = oracle.forward_warping_lexmin(obj, sy, sx, depth)
+            assert np.array_equal(lo, out) and np.array_equal(lv, valid) and np.array_equal(lc, coll), name
+        cases.update({f"{name}/obj": obj, f"{name}/safe_y": sy, f"{name}/safe_x": sx, f"{name}/depth": depth,
+                      f"{name}/output": out, f"{name}/valid": valid, f"{name}/collision": coll})
+    return cases
+
+
+def make_wrapper_cases(ref_fw):
+    """Drive the reference FW.forward (3-D inputs, as preprocess.py does)."""
+    rng = np.random.default_rng(99)
+    fw = ref_fw.FW("cpu")
+    cases = {}
+    specs = [
+        ("f32_c6", 6, 24, 32, torch.float32, 6.0),
+        ("f32_c2_big", 2, 20, 28, torch.float32, 60.0),
+        ("f64flow_c6", 6, 24, 32, torch.float64, 6.0),
+        ("f64obj_c4", 4, 16, 24, torch.float64, 3.0),
+    ]
+    for name, C, H, W, fdt, scale in specs:
+        obj = torch.from_numpy(rng.standard_normal((C, H, W))).to(torch.float64 if "f64obj" in name else torch.float32)
+        flow = torch.from_numpy(rng.standard_normal((2, H, W)) * scale).to(fdt)
+        depth = torch.from_numpy(rng.integers(1, 6, (1, H, W)).astype(np.float64)).to(fdt)
+        out, valid, coll = fw(obj, flow, depth)
+        cases.update({f"{name}/obj": obj.numpy(), f"{name}/flow": flow.numpy(), f"{name}/depth": depth.numpy(),
+                      f"{name}/output": out.numpy(), f"{name}/valid": valid.numpy(), f"{name}/collision": coll.numpy()})
+    # float64 flow within rounding of an integer: add done in float64 (fw.py:31)
+    H, W = 4, 8
+    flow = torch.zeros(2, H, W, dtype=torch.float64)
+    flow[0] = 0.99999999
+    flow[1, 1] = -0.99999999
+    flow[1, 2] = 1.0 - 1e-9
+    obj = torch.arange(3 * H * W, dtype=torch.float32).reshape(3, H, W)
+    depth = torch.ones(1, H, W, dtype=torch.float64)
+    out, valid, coll = fw(obj, flow, depth)
+    cases.update({"nearint_f64/obj": obj.numpy(), "nearint_f64/flow": flow.numpy(),
+                  "nearint_f64/depth": depth.numpy(), "nearint_f64/output": out.numpy(),
+                  "nearint_f64/valid": valid.numpy(), "nearint_f64/collision": coll.numpy()})
+    return cases
+
+
+def make_pipeline_cases(ref_fw, Plausible, Convert, utils_mod):
+    """preprocess.py:348-359 / :372-374 first-stage calls on synthetic depth."""
+    fw = ref_fw.FW("cpu")
+    cases = {}
+    for k, (h, w) in enumerate([(48, 64), (60, 80)]):
+        seed = 12345 + k
+        depth_np = synth_depth(h, w, seed)
+        rgb = torch.from_numpy(synth_rgb(h, w, seed))
+        # (a) disparity flow, depth float64 as utils.get_depth returns it (utils.py:47-59)
+        utils_mod.set_seed(seed)
+        d0 = utils_mod.normalize_depth(torch.from_numpy(depth_np.copy()).unsqueeze(0))
+        disp0 = Convert.depth_to_disparity(d0)
+        flow01 = Convert.disparity_to_flow(disp0, device="cpu", random_sign=False)
+        img0_all = torch.cat((rgb, d0, flow01 * -1.0), axis=0)       # preprocess.py:358
+        o, v, c = fw(img0_all, flow01, d0)                            # preprocess.py:359
+        # (b) ego-motion flow on float32 depth (preprocess.py:372, 385)
+        utils_mod.set_seed(seed + 7)
+        d0f = d0.to(torch.float32)
+        flow03, T1 = Convert.depth_to_random_flow(d0f, "cpu")
+        img0_all3 = torch.cat((rgb, d0f, flow03 * -1.0), axis=0)      # preprocess.py:386
+        o3, v3, c3 = fw(img0_all3, flow03, d0f)                       # preprocess.py:387
+        fixed = utils_mod.fix_warped_depth((o3[3:4] * v3).clone())    # preprocess.py:391,394
+        p = f"img{k}"
+        cases.update({
+            f"{p}/raw_depth": depth_np, f"{p}/rgb": rgb.numpy(), f"{p}/seed": np.array(seed),
+            f"{p}/norm_depth": d0.numpy(), f"{p}/flow01": flow01.numpy(),
+            f"{p}/fw01_output": o.numpy(), f"{p}/fw01_valid": v.numpy(), f"{p}/fw01_collision": c.numpy(),
+            f"{p}/T1": T1.numpy(), f"{p}/flow03": flow03.numpy(),
+            f"{p}/fw03_output": o3.numpy(), f"{p}/fw03_valid": v3.numpy(), f"{p}/fw03_collision": c3.numpy(),
+            f"{p}/fw03_fixed_depth": fixed.numpy(),
+        })
+    # Plausible.K and a batch of camera parameters drawn from the reference RNG
+    K, invK = Plausible.K((768, 1024))
+    cases["K_768x1024"] = K.numpy()
+    cases["invK_768x1024"] = invK.numpy()
+    Ts, ss = [], []
+    for i in range(8):
+        utils_mod.set_seed(12345 + i)
+        s = utils_mod.get_random(0.3, 0.8, random_sign=False)
+        T, _, _ = Plausible.random_motion(1. / 36., 1. / 36., 0.1, 0.1)
+        ss.append(float(s))
+        Ts.append(T.numpy()[0])
+    cases["camera_seeds"] = np.arange(12345, 12353)
+    cases["camera_s"] = np.array(ss, np.float32)
+    cases["camera_T"] = np.stack(Ts)
+    return cases
+
+
+def main():
+    ref_fw = load_reference_fw()
+    geometry_mod = load_reference_geometry()
+    utils_mod = load_reference_utils_subset()
+    Plausible, Convert = load_reference_plausible_convert(utils_mod, geometry_mod)
+
+    op = make_op_cases()
+    np.savez_compressed(os.path.join(HERE, "fw_op.npz"), **op)
+    wr = make_wrapper_cases(ref_fw)
+    np.savez_compressed(os.path.join(HERE, "fw_wrapper.npz"), **wr)
+    pl = make_pipeline_cases(ref_fw, Plausible, Convert, utils_mod)
+    np.savez_compressed(os.path.join(HERE, "pipeline.npz"), **pl)
+    for f in ("fw_op.npz", "fw_wrapper.npz", "pipeline.npz"):
+        print(f, os.path.getsize(os.path.join(HERE, f)), "bytes")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,110 @@
+"""CPU tests of the C-ABI library and the host-side boundary (no compute calls)."""
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+
+from conftest import REPO
+
+
+def _header_symbols():
+    txt = open(os.path.join(REPO, "include", "ofd_fw.h")).read()
+    return sorted(set(re.findall(r"\b(ofd_fw_\w+)\s*\(", txt)))
+
+
+def test_library_exports_every_header_symbol():
+    from opticalflowfromdepth_amd import _native
+    lib = _native.lib()
+    syms = _header_symbols()
+    assert len(syms) >= 8
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert set(syms) == set(_native.SIGNATURES)
+
+
+def test_library_is_gfx950_code_object():
+    from opticalflowfromdepth_amd import _native
+    _native.lib()
+    data = open(_native.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+
+
+def test_abi_and_strerror():
+    from opticalflowfromdepth_amd import _native
+    lib = _native.lib()
+    assert lib.ofd_fw_abi_version() == _native.ABI_VERSION
+    for rc in (0, -1, -2, -3, -4):
+        assert lib.ofd_fw_strerror(rc)
+
+
+def test_workspace_bytes():
+    from opticalflowfromdepth_amd import _native
+    lib = _native.lib()
+    hw = 768 * 1024
+    b = lib.ofd_fw_workspace_bytes(64, 768, 1024, 0)
+    assert b % (hw * 8) == 0 and 1 <= b // (hw * 8) <= 64
+    assert lib.ofd_fw_workspace_bytes(1, 768, 1024, 0) == hw * 8
+    assert lib.ofd_fw_workspace_bytes(2, 4, 4, 1) == 2 * 16 * 12
+    assert lib.ofd_fw_workspace_bytes(0, 4, 4, 0) == 0
+
+
+def test_argument_errors_without_gpu():
+    """Validation happens before any HIP call, so it is testable on CPU."""
+    from opticalflowfromdepth_amd import _native
+    lib = _native.lib()
+    # negative dimension
+    assert lib.ofd_fw_forward_warping_f32(*([None] * 7), -1, 1, 1, 1, None, 0, None) == -1
+    # H*W >= 2^31
+    assert lib.ofd_fw_forward_warp_flow_f32(*([None] * 6), 1, 1, 1 << 16, 1 << 15, None, 0, None) == -2
+    # empty batch is a no-op success
+    assert lib.ofd_fw_forward_warp_flow_f32(*([None] * 6), 0, 6, 4, 4, None, 0, None) == 0
+    # null pointers with work to do
+    assert lib.ofd_fw_forward_warp_flow_f32(*([None] * 6), 1, 6, 4, 4, None, 0, None) == -1
+
+
+def test_ops_reject_cpu_tensors_like_reference():
+    import fw_cuda
+    from opticalflowfromdepth_amd import FW
+    t = torch.zeros(1, 1, 2, 2)
+    with pytest.raises(RuntimeError, match="obj must be a CUDA tensor"):
+        fw_cuda.forward_warping(t, t, t, t)
+    with pytest.raises(RuntimeError, match="must be a CUDA tensor"):
+        FW()(torch.zeros(3, 2, 2), torch.zeros(2, 2, 2), torch.zeros(1, 2, 2))
+
+
+def test_drop_in_module_surface():
+    import alt_cuda.fw as afw
+    import fw_cuda
+    from opticalflowfromdepth_amd import FW
+    assert afw.FW is FW
+    m = FW("cuda:0")
+    assert isinstance(m, torch.nn.Module) and m.device == "cuda:0"
+    assert list(m.parameters()) == [] and list(m.buffers()) == []
+    assert callable(fw_cuda.forward_warping)
+
+
+def test_product_never_imports_oracle():
+    """The product path must not route through the test oracle."""
+    pkg = os.path.join(REPO, "opticalflowfromdepth_amd")
+    for root, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".hip", ".cpp", ".h")):
+                src = open(os.path.join(root, f)).read()
+                assert "import oracle" not in src and "from oracle" not in src, f
+                assert "fw_oracle" not in src, f
+    for f in ("fw_cuda.py", os.path.join("alt_cuda", "fw.py")):
+        src = open(os.path.join(REPO, f)).read()
+        assert "oracle" not in src
+
+
+def test_c_abi_header_compiles_as_c():
+    """include/ofd_fw.h is plain C (no HIP / torch types)."""
+    import subprocess
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "t.c")
+        open(c, "w").write('#include "ofd_fw.h"\nint main(void){int (*f)(void) = ofd_fw_abi_version; (void)f; return OFD_FW_OK;}\n')
+        subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-c", "-I", os.path.join(REPO, "include"),
+                        c, "-o", os.path.join(d, "t.o")], check=True)
