@@ -46,6 +46,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline wall budget")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
     ap.add_argument("--check", action="store_true", help="verify one image against the oracle")
+    ap.add_argument("--engine", choices=["tile", "atomic"], default="tile")
     return ap.parse_args()
 
 
@@ -100,7 +101,7 @@ def main():
                                              camera=(s_all[a:b], T_all[a:b]))
     C = obj.shape[1]
     out = (torch.empty_like(obj), torch.empty_like(depth), torch.empty_like(depth))
-    _native.lib()
+    _native.lib().ofd_fw_set_engine(0 if args.engine == "tile" else 1)
     torch.cuda.synchronize()
 
     for _ in range(args.warmup):
@@ -178,7 +179,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
-                         "kernel": "ofd_fw forward_warp_flow (splat + resolve launches of one call)",
+                         "kernel": f"ofd_fw forward_warp_flow, {args.engine} engine (all launches of one call)",
                          "algorithmic_bytes_per_px": bytes_per_px,
                          "event_ms_per_call": round(dev_ms, 4),
                          "traffic_source": traffic_note},

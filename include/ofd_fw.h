@@ -59,6 +59,15 @@ enum {
 /* ABI version of the loaded library (OFD_FW_ABI_VERSION at build time). */
 int ofd_fw_abi_version(void);
 
+/* Engines (see csrc/ofd_fw.hip): TILE = LDS z-buffer per target tile (default);
+ * ATOMIC = one global 64-bit atomic min per source.  Results are identical.
+ * Selects the engine for subsequent calls in this process (also settable with
+ * OFD_FW_MODE=atomic); an unknown value only queries.  Returns the previous
+ * engine.  Not thread-safe against concurrent calls. */
+#define OFD_FW_ENGINE_TILE 0
+#define OFD_FW_ENGINE_ATOMIC 1
+int ofd_fw_set_engine(int engine);
+
 /* Human-readable name of a return code (static storage). */
 const char *ofd_fw_strerror(int code);
 

@@ -1,32 +1,50 @@
 // ofd_fw.hip -- MI355X (gfx950) forward-warp engine: z-buffered splat + resolve.
 //
 // Replaces the reference's single-workgroup serial kernel
-// (alt_cuda/fw_cuda_kernel.cu:9-49, grid <<<B, C>>>, one thread walks all H*W
-// sources of one (image, channel)) with a data-parallel two-phase design:
+// (alt_cuda/fw_cuda_kernel.cu:9-49: grid <<<B, C>>>, one thread walks all H*W
+// sources of one (image, channel)) with data-parallel kernels.  The z-test is
+// restated as a lexicographic minimum: every source s landing on target t
+// with depth < 1000 offers the 64-bit key
+//       key(s) = orderable(depth[s]) << 32 | s          (s = raster index j*W+i)
+// and the winner of t is the source with the smallest key -- exactly the
+// source the reference's raster loop keeps with its strict `<` (ties keep the
+// earliest source).  Sources with depth >= 1000 or NaN
+// offer KEY_NOWIN, which marks the target valid without a winner (the
+// reference's collision = 1 case, fw_cuda_kernel.cu:38-45).  The min is
+// commutative, so the result is bit-identical however the work is scheduled.
 //
-//   splat   : one lane per source pixel.  Computes the target pixel (from the
-//             flow, fw.py:27-42 fused in, or from given safe coordinates) and
-//             folds a 64-bit key  (orderable(depth) << 32) | raster_index  into
-//             the target's slot with one native 64-bit atomic min
-//             (global_atomic_umin_x2).  Sources with depth >= 1000 / NaN mark
-//             the slot "touched, no winner" (KEY_NOWIN) so valid/collision are
-//             reproduced.  The lexicographic (depth, raster index) minimum is
-//             exactly the winner of the reference's raster loop with its strict
-//             `<` (ties keep the earliest source): SURVEY.md 0.1 item 1.
-//   resolve : one lane per target pixel.  Reads the key, gathers the winner's C
-//             channel values, writes output / valid / collision exactly once
-//             (16-byte stores), and resets the key slot to KEY_UNTOUCHED so the
-//             workspace needs no clearing pass before the next call.
+// Two engines share the key algebra:
 //
-// Images are processed in chunks whose key slab fits the workspace the caller
-// passes (ofd_fw_workspace_bytes suggests a slab that stays resident in the
-// 256 MiB Infinity Cache, so the key traffic does not reach HBM).
+//  TILE (default).  Targets are cut into TW x TH tiles whose z-buffer lives in
+//  LDS (ds_min_u64 is ~25x the chip rate of a global 64-bit atomic min,
+//  tools/microbench.hip).  Sources are cut into 64-pixel blocks (one wave).
+//    bin  : one wave per source block computes its targets' bounding box and
+//           appends the block id to the list of every tile the box overlaps
+//           (one global atomic per (block, tile), ~1.4 per block).
+//    tile : one workgroup per target tile re-reads the listed source blocks
+//           (a cache-resident re-read when the batch is processed in chunks),
+//           folds their keys into the LDS z-buffer, then resolves: gathers the
+//           winners' C channels and writes output / valid / collision once,
+//           16-byte stores, no scratch traffic to HBM.
+//    Blocks whose box spans too many tiles (non-smooth flow) and list overflow
+//    (border hot spots) fall back to global atomics on a per-image key slab
+//    (pre-reduced over runs of equal targets inside the wave); the tile kernel
+//    merges that slab for flagged tiles only.
 //
-// Everything here is plain HIP for gfx950; no CUDA compatibility layer.
+//  ATOMIC (OFD_FW_MODE=atomic; and the float64 op).  One global 64-bit atomic
+//  min per source into a per-image key slab, then a resolve pass.
+//
+// Workspace invariant: every call leaves the caller's workspace bytes all-ones
+// (keys = KEY_UNTOUCHED, tile counters encoded as ~count, flags ~0), so the
+// workspace is initialised once (ofd_fw_workspace_init) and never cleared.
+//
+// Plain HIP for gfx950; no CUDA compatibility layer, no dual paths.
 
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
 
 #include "ofd_fw.h"
 
@@ -35,14 +53,21 @@ namespace {
 constexpr int kBlock = 256;
 constexpr unsigned long long KEY_UNTOUCHED = ~0ull;                 // no source landed
 constexpr unsigned long long KEY_NOWIN = 0xFFFFFFFF00000000ull;     // landed, none < 1000
-// f64 op: depth keys are full 64-bit orderable doubles, index kept aside
-constexpr unsigned long long ZKEY_UNTOUCHED = ~0ull;
+constexpr unsigned long long ZKEY_UNTOUCHED = ~0ull;                // f64 op depth keys
 constexpr unsigned long long ZKEY_NOWIN = ~0ull - 1ull;
 constexpr unsigned int IDX_NONE = ~0u;
 
-// Default key slab: 8 images of 768x1024 (48 MiB) -- resident in the MALL
-// together with the chunk's streamed planes.
-constexpr size_t kDefaultSlabBytes = size_t(48) << 20;
+// tile engine geometry
+constexpr int TW = 128, TH = 32;          // target tile (LDS z-buffer 32 KiB)
+constexpr int SBW = 16, SBH = 4;          // source block = one wave (64 px)
+constexpr int CAP = 256;                  // list entries per tile before overflow
+constexpr int MAX_TILES_PER_BLOCK = 12;   // wider boxes go through the global path
+constexpr int kUnroll = 4;                // source pixels in flight per thread
+
+// Default chunk: 4 images of 768x1024 (26 MB of slab); a chunk's re-read
+// flow/depth planes (12 B/px) stay resident in the 256 MiB Infinity Cache
+// between its BIN and TILE roles.
+constexpr size_t kDefaultChunkBytes = size_t(26) << 20;
 
 // ---------------------------------------------------------------- key helpers
 // Monotone map float -> uint32 (total order of non-NaN floats), -0 == +0.
@@ -68,46 +93,39 @@ __device__ __forceinline__ unsigned long long make_key(float d, unsigned int src
 // Op level: coordinates as given to fw_cuda.forward_warping.  The reference
 // indexes its accessor with them, i.e. converts float -> int32 by truncation
 // (fw_cuda_kernel.cu:31-35); an out-of-range index is UB there and a dropped
-// source here.
+// source (tx = -1) here.
 template <typename T>
-__device__ __forceinline__ int target_safe(T x, T y, int H, int W) {
-    if (!(x > T(-1)) || !(x < T(W)) || !(y > T(-1)) || !(y < T(H))) return -1;
-    return int(y) * W + int(x);
+__device__ __forceinline__ void target_safe(T x, T y, int H, int W, int &tx, int &ty) {
+    if (!(x > T(-1)) || !(x < T(W)) || !(y > T(-1)) || !(y < T(H))) { tx = ty = -1; return; }
+    tx = int(x);
+    ty = int(y);
 }
 
 // FW level: fw.py:27-42.  p1 = p0 + flow in the flow's dtype (p0 is the
 // float32 meshgrid, exact for any pixel index < 2^24), clamp to [0, W-1] x
 // [0, H-1], truncate through int64.  NaN survives torch.clamp and is dropped.
 template <typename F>
-__device__ __forceinline__ int target_flow(int i, int j, F fx, F fy, int H, int W) {
+__device__ __forceinline__ void target_flow(int i, int j, F fx, F fy, int H, int W, int &tx, int &ty) {
     F px = F(i) + fx;
     F py = F(j) + fy;
-    if (px != px || py != py) return -1;
+    if (px != px || py != py) { tx = ty = -1; return; }
     px = px < F(0) ? F(0) : (px > F(W - 1) ? F(W - 1) : px);
     py = py < F(0) ? F(0) : (py > F(H - 1) ? F(H - 1) : py);
-    return int(py) * W + int(px);
+    tx = int(px);
+    ty = int(py);
 }
 
-// Coordinate sources.  load<VEC>() fetches the raw per-source values of VEC
-// consecutive sources (vectorised when VEC == 4), target() maps one of them.
+// Coordinate sources: the target of the source at pixel p = j*W + i of image b.
 struct SafeF32 {  // fw_cuda.forward_warping inputs: safe_y, safe_x [B,1,H,W]
     using V = float;
     const float *sy, *sx;
     int64_t HW;
-    template <int VEC>
-    __device__ __forceinline__ void load(int64_t g, int64_t, V (&x)[VEC], V (&y)[VEC]) const {
-        if constexpr (VEC == 4) {
-            const float4 a = *reinterpret_cast<const float4 *>(sx + g);
-            const float4 c = *reinterpret_cast<const float4 *>(sy + g);
-            x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
-            y[0] = c.x; y[1] = c.y; y[2] = c.z; y[3] = c.w;
-        } else {
-#pragma unroll
-            for (int k = 0; k < VEC; ++k) { x[k] = sx[g + k]; y[k] = sy[g + k]; }
-        }
+    __device__ __forceinline__ void load(int64_t b, int64_t p, V &x, V &y) const {
+        x = sx[b * HW + p];
+        y = sy[b * HW + p];
     }
-    __device__ __forceinline__ int target(int, int, V x, V y, int H, int W) const {
-        return target_safe<float>(x, y, H, W);
+    __device__ __forceinline__ void target(int, int, V x, V y, int H, int W, int &tx, int &ty) const {
+        target_safe<float>(x, y, H, W, tx, ty);
     }
 };
 
@@ -116,140 +134,495 @@ struct FlowCoords {  // FW.forward input: flow [B,2,H,W], ch0 = x, ch1 = y
     using V = F;
     const F *flow;
     int64_t HW;
-    template <int VEC>
-    __device__ __forceinline__ void load(int64_t, int64_t bp, V (&x)[VEC], V (&y)[VEC]) const {
-        // bp = b*2*HW + p: the x plane sample; the y plane is HW further on
-        const F *fx = flow + bp;
-        const F *fy = fx + HW;
-        if constexpr (VEC == 4 && sizeof(F) == 4) {
-            const float4 a = *reinterpret_cast<const float4 *>(fx);
-            const float4 c = *reinterpret_cast<const float4 *>(fy);
-            x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
-            y[0] = c.x; y[1] = c.y; y[2] = c.z; y[3] = c.w;
-        } else if constexpr (VEC == 4 && sizeof(F) == 8) {
-            const double2 a0 = *reinterpret_cast<const double2 *>(fx);
-            const double2 a1 = *reinterpret_cast<const double2 *>(fx + 2);
-            const double2 c0 = *reinterpret_cast<const double2 *>(fy);
-            const double2 c1 = *reinterpret_cast<const double2 *>(fy + 2);
-            x[0] = a0.x; x[1] = a0.y; x[2] = a1.x; x[3] = a1.y;
-            y[0] = c0.x; y[1] = c0.y; y[2] = c1.x; y[3] = c1.y;
-        } else {
-#pragma unroll
-            for (int k = 0; k < VEC; ++k) { x[k] = fx[k]; y[k] = fy[k]; }
-        }
+    __device__ __forceinline__ void load(int64_t b, int64_t p, V &x, V &y) const {
+        const F *f = flow + b * 2 * HW + p;
+        x = f[0];
+        y = f[HW];
     }
-    __device__ __forceinline__ int target(int i, int j, V x, V y, int H, int W) const {
-        return target_flow<F>(i, j, x, y, H, W);
+    __device__ __forceinline__ void target(int i, int j, V x, V y, int H, int W, int &tx, int &ty) const {
+        target_flow<F>(i, j, x, y, H, W, tx, ty);
     }
 };
 
-// ---------------------------------------------------------------- splat (f32 depth)
-// One thread handles VEC consecutive sources of one image (HW % VEC == 0).
-// Runs of equal targets inside the thread (border clamping, flat regions)
-// are merged before touching memory.
-template <int VEC, typename Coords>
-__global__ __launch_bounds__(kBlock) void splat_f32_kernel(
-        Coords co, const float *__restrict__ depth, unsigned long long *__restrict__ keys,
-        int H, int W, int64_t HW, int64_t b0, int64_t chunk_px) {
-    const int64_t q = (int64_t(blockIdx.x) * kBlock + threadIdx.x) * VEC;  // chunk-local
-    if (q >= chunk_px) return;
-    const int64_t bl = q / HW;
-    const int64_t p = q - bl * HW;  // pixel in image
-    const int64_t b = b0 + bl;
-    const int64_t g = b * HW + p;   // global plane index
+// ---------------------------------------------------------------- wave helpers
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
-    float d[VEC];
-    if constexpr (VEC == 4) {
-        const float4 v = *reinterpret_cast<const float4 *>(depth + g);
-        d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
-    } else {
+__device__ __forceinline__ int wave_min(int v) {
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) d[k] = depth[g + k];
-    }
-    typename Coords::V cx[VEC], cy[VEC];
-    co.template load<VEC>(g, b * 2 * HW + p, cx, cy);
-    int j = int(p / W);
-    int i = int(p - int64_t(j) * W);
-    unsigned long long *kb = keys + bl * HW;
-
-    int run_t = -1;
-    unsigned long long run_key = KEY_UNTOUCHED;
+    for (int d = 32; d >= 1; d >>= 1) { const int o = __shfl_xor(v, d); v = o < v ? o : v; }
+    return v;
+}
+__device__ __forceinline__ int wave_max(int v) {
 #pragma unroll
-    for (int k = 0; k < VEC; ++k) {
-        const int t = co.target(i, j, cx[k], cy[k], H, W);
-        const unsigned long long key = make_key(d[k], (unsigned int)(p + k));
-        if (t != run_t) {
-            if (run_t >= 0) atomicMin(kb + run_t, run_key);
-            run_t = t;
-            run_key = key;
-        } else if (key < run_key) {
-            run_key = key;
-        }
-        if (++i == W) { i = 0; ++j; }
-    }
-    if (run_t >= 0) atomicMin(kb + run_t, run_key);
+    for (int d = 32; d >= 1; d >>= 1) { const int o = __shfl_xor(v, d); v = o > v ? o : v; }
+    return v;
 }
 
-// ---------------------------------------------------------------- resolve (f32)
-template <int VEC>
-__global__ __launch_bounds__(kBlock) void resolve_f32_kernel(
-        const float *__restrict__ obj, unsigned long long *__restrict__ keys,
-        float *__restrict__ out, float *__restrict__ valid, float *__restrict__ coll,
-        int C, int64_t HW, int64_t b0, int64_t chunk_px) {
-    const int64_t q = (int64_t(blockIdx.x) * kBlock + threadIdx.x) * VEC;
-    if (q >= chunk_px) return;
-    const int64_t bl = q / HW;
-    const int64_t p = q - bl * HW;
-    const int64_t b = b0 + bl;
-
-    unsigned long long key[VEC];
-    if constexpr (VEC == 4) {
-        const ulonglong2 k01 = *reinterpret_cast<const ulonglong2 *>(keys + q);
-        const ulonglong2 k23 = *reinterpret_cast<const ulonglong2 *>(keys + q + 2);
-        key[0] = k01.x; key[1] = k01.y; key[2] = k23.x; key[3] = k23.y;
-        const ulonglong2 ones = {KEY_UNTOUCHED, KEY_UNTOUCHED};
-        *reinterpret_cast<ulonglong2 *>(keys + q) = ones;
-        *reinterpret_cast<ulonglong2 *>(keys + q + 2) = ones;
-    } else {
+// Global atomic min of `key` into base[t] for every lane with t >= 0, issuing
+// one atomic per run of consecutive lanes with the same t (border clamping
+// sends long runs to one pixel).  Segmented inclusive min-scan over the runs;
+// every lane of the wave must call it.
+__device__ __forceinline__ void wave_run_atomic_min(unsigned long long *base, int t, unsigned long long key) {
+    const int lane = lane_id();
+    const int tprev = __shfl_up(t, 1);
+    const bool head = lane == 0 || tprev != t;
+    const unsigned long long heads = __ballot(head);
+    const unsigned long long le = lane == 63 ? ~0ull : ((1ull << (lane + 1)) - 1ull);
+    const int seg_start = 63 - __clzll(heads & le);
+    unsigned int lo = (unsigned int)key, hi = (unsigned int)(key >> 32);
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) { key[k] = keys[q + k]; keys[q + k] = KEY_UNTOUCHED; }
+    for (int d = 1; d < 64; d <<= 1) {
+        const unsigned int olo = __shfl_up(lo, d), ohi = __shfl_up(hi, d);
+        if (lane - d >= seg_start) {
+            const unsigned long long o = ((unsigned long long)ohi << 32) | olo;
+            const unsigned long long k = ((unsigned long long)hi << 32) | lo;
+            if (o < k) { lo = olo; hi = ohi; }
+        }
     }
+    const int tnext = __shfl_down(t, 1);
+    const bool tail = lane == 63 || tnext != t;
+    if (tail && t >= 0) atomicMin(base + t, ((unsigned long long)hi << 32) | lo);
+}
 
-    int src[VEC];
-    float vv[VEC], cc[VEC];
+// ---------------------------------------------------------------- workspace layout
+struct TileGeom {
+    int tilesX, tilesY, ntiles;  // target tiles per image
+    int nsbx, nsby, nsb;         // source blocks per image
+};
+
+inline TileGeom make_geom(int64_t H, int64_t W) {
+    TileGeom g;
+    g.tilesX = int((W + TW - 1) / TW);
+    g.tilesY = int((H + TH - 1) / TH);
+    g.ntiles = g.tilesX * g.tilesY;
+    g.nsbx = int((W + SBW - 1) / SBW);
+    g.nsby = int((H + SBH - 1) / SBH);
+    g.nsb = g.nsbx * g.nsby;
+    return g;
+}
+
+// Per-image workspace: key slab (HW u64) + tile counters + flags + lists.
+inline size_t per_image_bytes(int64_t H, int64_t W) {
+    const TileGeom g = make_geom(H, W);
+    return size_t(H) * size_t(W) * 8 + size_t(g.ntiles) * (8 + size_t(CAP) * 4);
+}
+
+struct Ws {  // views of one chunk's workspace (G images)
+    unsigned long long *keys;  // [G][HW]
+    unsigned int *cnt;         // [G][ntiles], ~count
+    unsigned int *flag;        // [G][ntiles], 0 = merge key slab, ~0 = clean
+    unsigned int *list;        // [G][ntiles][CAP]
+};
+
+inline Ws carve(void *ws, int64_t G, int64_t HW, const TileGeom &g) {
+    Ws w;
+    char *p = static_cast<char *>(ws);
+    w.keys = reinterpret_cast<unsigned long long *>(p);
+    p += size_t(G) * size_t(HW) * 8;
+    w.cnt = reinterpret_cast<unsigned int *>(p);
+    p += size_t(G) * g.ntiles * 4;
+    w.flag = reinterpret_cast<unsigned int *>(p);
+    p += size_t(G) * g.ntiles * 4;
+    w.list = reinterpret_cast<unsigned int *>(p);
+    return w;
+}
+
+// ---------------------------------------------------------------- TILE engine
+// One fused, pipelined kernel per chunk boundary: launch L runs the TILE role
+// for chunk L-1 and the BIN role for chunk L side by side (their workspace
+// slabs alternate), so the latency-bound binning hides under the streaming
+// tile resolve.  Roles are interleaved evenly over the grid.
+constexpr int kWarpThreads = 512;
+constexpr int kWaves = kWarpThreads / 64;
+constexpr int kBinBlocks = kWaves * 4;                         // 4 source blocks per wave
+constexpr int kMaxRegs = kBinBlocks * MAX_TILES_PER_BLOCK;     // (block, tile) registrations
+
+struct BinLds {
+    int box[kBinBlocks][4];  // tile range t0x,t1x,t0y,t1y; t0x = -1 empty, -2 wide
+    int img[kBinBlocks], sb[kBinBlocks];
+    int off[kBinBlocks + 1];
+    int reg_tile[kMaxRegs];  // chunk-global tile id (image * ntiles + tile)
+    unsigned int base[kMaxRegs];
+    unsigned int slot[kMaxRegs];
+    unsigned char reg_blk[kMaxRegs];
+};
+
+struct TileLds {
+    unsigned long long zk[TW * TH];
+    unsigned int list[CAP];
+    unsigned int n, flag;
+};
+
+union __align__(16) WarpLds {
+    BinLds bin;
+    TileLds tile;
+};
+
+struct ChunkArgs {  // one chunk's share of a launch
+    Ws ws;
+    int64_t b0;     // first image of the chunk
+    int nimg;       // images in the chunk
+    int nwg;        // workgroups of this role in the launch
+};
+
+// ---- BIN role: kBinBlocks consecutive source blocks per workgroup.  Each
+// wave computes its blocks' target bounding boxes; the workgroup aggregates
+// the (block, tile) registrations in LDS so each distinct tile costs ONE
+// returning global atomic per workgroup (all issued together), then writes the
+// list entries.  Registrations past a tile's CAP and blocks whose box spans
+// more than MAX_TILES_PER_BLOCK tiles spill to the key slab.
+template <typename Coords>
+__device__ __forceinline__ void bin_role(BinLds &L, int wg, const Coords &co, const float *__restrict__ depth,
+                                         const ChunkArgs &a, int H, int W, int64_t HW, const TileGeom &g) {
+    const Ws &ws = a.ws;
+    const int lane = lane_id(), wave = threadIdx.x >> 6;
+    const int64_t nblk = int64_t(a.nimg) * g.nsb;
+    int tx[4], ty[4];
 #pragma unroll
-    for (int k = 0; k < VEC; ++k) {
-        const bool touched = key[k] != KEY_UNTOUCHED;
-        const bool nowin = key[k] == KEY_NOWIN;
-        vv[k] = touched ? 1.f : 0.f;
-        cc[k] = nowin ? 1.f : 0.f;
-        src[k] = (touched && !nowin) ? int(key[k] & 0xFFFFFFFFull) : -1;
+    for (int k = 0; k < 4; ++k) {
+        const int kk = wave * 4 + k;
+        const int64_t sbg = int64_t(wg) * kBinBlocks + kk;
+        tx[k] = ty[k] = -1;
+        if (sbg < nblk) {
+            const int bl = int(sbg / g.nsb);
+            const int sb = int(sbg - int64_t(bl) * g.nsb);
+            const int sby = sb / g.nsbx, sbx = sb - sby * g.nsbx;
+            const int i = sbx * SBW + (lane % SBW), j = sby * SBH + (lane / SBW);
+            if (lane == 0) { L.img[kk] = bl; L.sb[kk] = sb; }
+            if (i < W && j < H) {
+                typename Coords::V x, y;
+                co.load(a.b0 + bl, int64_t(j) * W + i, x, y);
+                co.target(i, j, x, y, H, W, tx[k], ty[k]);
+            }
+        } else if (lane == 0) {
+            L.img[kk] = -1;
+        }
     }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const bool ok = tx[k] >= 0;
+        const int mnx = wave_min(ok ? tx[k] : 0x7FFFFFFF), mxx = wave_max(ok ? tx[k] : -1);
+        const int mny = wave_min(ok ? ty[k] : 0x7FFFFFFF), mxy = wave_max(ok ? ty[k] : -1);
+        if (lane == 0) {
+            const int kk = wave * 4 + k;
+            if (mxx < 0) {
+                L.box[kk][0] = -1;
+            } else {
+                const int t0x = mnx / TW, t1x = mxx / TW, t0y = mny / TH, t1y = mxy / TH;
+                const bool wide = (t1x - t0x + 1) * (t1y - t0y + 1) > MAX_TILES_PER_BLOCK;
+                L.box[kk][0] = wide ? -2 : t0x;
+                L.box[kk][1] = t1x;
+                L.box[kk][2] = t0y;
+                L.box[kk][3] = t1y;
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int off = 0;
+        for (int k = 0; k < kBinBlocks; ++k) {
+            L.off[k] = off;
+            if (L.box[k][0] >= 0) off += (L.box[k][1] - L.box[k][0] + 1) * (L.box[k][3] - L.box[k][2] + 1);
+        }
+        L.off[kBinBlocks] = off;
+    }
+    __syncthreads();
+    if (threadIdx.x < kBinBlocks && L.box[threadIdx.x][0] >= 0) {
+        const int k = threadIdx.x;
+        int r = L.off[k];
+        for (int yt = L.box[k][2]; yt <= L.box[k][3]; ++yt)
+            for (int xt = L.box[k][0]; xt <= L.box[k][1]; ++xt, ++r) {
+                L.reg_tile[r] = L.img[k] * g.ntiles + yt * g.tilesX + xt;
+                L.reg_blk[r] = (unsigned char)k;
+            }
+    }
+    __syncthreads();
+    const int nreg = L.off[kBinBlocks];
+    int first = 0, rank = 0;
+    if (int(threadIdx.x) < nreg) {
+        const int r = threadIdx.x, T = L.reg_tile[r];
+        int tot = 0;
+        first = r;
+        for (int q = 0; q < nreg; ++q) {
+            if (L.reg_tile[q] == T) {
+                ++tot;
+                if (q < r) { ++rank; first = q < first ? q : first; }
+            }
+        }
+        if (rank == 0) L.base[r] = 0xFFFFFFFFu - atomicSub(ws.cnt + T, unsigned(tot));
+    }
+    __syncthreads();
+    if (int(threadIdx.x) < nreg) {
+        const int r = threadIdx.x, T = L.reg_tile[r];
+        const unsigned slot = L.base[first] + unsigned(rank);
+        L.slot[r] = slot;
+        if (slot < unsigned(CAP)) ws.list[int64_t(T) * CAP + slot] = unsigned(L.sb[L.reg_blk[r]]);
+    }
+    __syncthreads();
+    // ---- spills: wide boxes and list overflow go through the key slab
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int kk = wave * 4 + k;
+        if (L.img[kk] < 0 || L.box[kk][0] == -1) continue;  // wave-uniform
+        const int bl = L.img[kk];
+        const int sb = L.sb[kk];
+        const int sby = sb / g.nsbx, sbx = sb - sby * g.nsbx;
+        const int i = sbx * SBW + (lane % SBW), j = sby * SBH + (lane / SBW);
+        const int64_t b = a.b0 + bl, p = int64_t(j) * W + i;
+        const bool ok = tx[k] >= 0;
+        const int mytile = ok ? bl * g.ntiles + (ty[k] / TH) * g.tilesX + tx[k] / TW : -1;
+        unsigned long long *keys = ws.keys + int64_t(bl) * HW;
+        if (L.box[kk][0] == -2) {
+            const unsigned long long key = ok ? make_key(depth[b * HW + p], unsigned(p)) : 0ull;
+            wave_run_atomic_min(keys, ok ? ty[k] * W + tx[k] : -1, key);
+            if (ok) ws.flag[mytile] = 0u;
+            continue;
+        }
+        for (int r = L.off[kk]; r < L.off[kk + 1]; ++r) {
+            if (L.slot[r] < unsigned(CAP)) continue;
+            const int T = L.reg_tile[r];
+            const bool mine = mytile == T;
+            const unsigned long long key = mine ? make_key(depth[b * HW + p], unsigned(p)) : 0ull;
+            wave_run_atomic_min(keys, mine ? ty[k] * W + tx[k] : -1, key);
+            if (lane == 0) ws.flag[T] = 0u;
+        }
+    }
+}
 
+// ---- TILE role: one workgroup per target tile.  Re-reads the listed source
+// blocks, folds their keys into the LDS z-buffer, merges the key slab if the
+// tile was flagged, then resolves the tile: gathers winners' channels and
+// writes output / valid / collision once with 16-byte stores.
+template <typename Coords>
+__device__ __forceinline__ void tile_role(TileLds &L, int lin, const Coords &co, const float *__restrict__ obj,
+                                          const float *__restrict__ depth, float *__restrict__ out,
+                                          float *__restrict__ valid, float *__restrict__ coll,
+                                          const ChunkArgs &a, int C, int H, int W, int64_t HW,
+                                          const TileGeom &g, int vec_ok) {
+    const Ws &ws = a.ws;
+    const int bl = lin / g.ntiles;
+    const int tile = lin - bl * g.ntiles;
+    const int tyi = tile / g.tilesX, txi = tile - tyi * g.tilesX;
+    const int x0 = txi * TW, y0 = tyi * TH;
+    const int64_t b = a.b0 + bl;
+    unsigned int *cnt = ws.cnt + lin;
+    unsigned int *flag = ws.flag + lin;
+    unsigned int *list = ws.list + int64_t(lin) * CAP;
+    unsigned long long *keys = ws.keys + int64_t(bl) * HW;
+
+    if (threadIdx.x == 0) {
+        const unsigned int c = 0xFFFFFFFFu - *cnt;
+        L.n = c < unsigned(CAP) ? c : unsigned(CAP);
+        L.flag = *flag;
+        *cnt = 0xFFFFFFFFu;  // restore the workspace invariant for the next call
+        *flag = 0xFFFFFFFFu;
+    }
+    for (int k = threadIdx.x; k < TW * TH; k += kWarpThreads) L.zk[k] = KEY_UNTOUCHED;
+    __syncthreads();
+    const int n = int(L.n);
+    for (int k = threadIdx.x; k < n; k += kWarpThreads) {
+        L.list[k] = list[k];
+        list[k] = 0xFFFFFFFFu;
+    }
+    __syncthreads();
+
+    // ---- splat the listed source blocks into the LDS z-buffer
+    const int items = n * 64;
+    for (int w0 = threadIdx.x; w0 < items; w0 += kWarpThreads * kUnroll) {
+        typename Coords::V cx[kUnroll], cy[kUnroll];
+        float d[kUnroll];
+        int ii[kUnroll], jj[kUnroll];
+        bool live[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const int it = w0 + u * kWarpThreads;
+            live[u] = false;
+            if (it < items) {
+                const int sb = int(L.list[it >> 6]);
+                const int l = it & 63;
+                const int sby = sb / g.nsbx, sbx = sb - sby * g.nsbx;
+                ii[u] = sbx * SBW + (l % SBW);
+                jj[u] = sby * SBH + (l / SBW);
+                if (ii[u] < W && jj[u] < H) {
+                    live[u] = true;
+                    const int64_t p = int64_t(jj[u]) * W + ii[u];
+                    co.load(b, p, cx[u], cy[u]);
+                    d[u] = depth[b * HW + p];
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            if (!live[u]) continue;
+            int tx, ty;
+            co.target(ii[u], jj[u], cx[u], cy[u], H, W, tx, ty);
+            const int lx = tx - x0, ly = ty - y0;
+            if (tx >= 0 && unsigned(lx) < unsigned(TW) && unsigned(ly) < unsigned(TH))
+                atomicMin(&L.zk[ly * TW + lx], make_key(d[u], unsigned(jj[u] * W + ii[u])));
+        }
+    }
+    // ---- merge the global key slab where the bin pass spilled into it
+    if (L.flag == 0u) {
+        for (int k = threadIdx.x; k < TW * TH; k += kWarpThreads) {
+            const int ly = k / TW, lx = k - ly * TW;
+            const int tx = x0 + lx, ty = y0 + ly;
+            if (tx < W && ty < H) {
+                unsigned long long *gk = keys + int64_t(ty) * W + tx;
+                const unsigned long long v = *gk;
+                if (v != KEY_UNTOUCHED) {
+                    atomicMin(&L.zk[k], v);
+                    *gk = KEY_UNTOUCHED;
+                }
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- resolve: each thread owns kSteps groups of 4 consecutive targets;
+    // the gathers of up to kChan channels are all issued before any store, so
+    // one memory round trip covers 4 targets x kChan channels.  Offsets are
+    // 32-bit from the image base (C*H*W < 2^30 is checked on the host).
+    constexpr int kSteps = TW * TH / 4 / kWarpThreads;  // 2
+    constexpr int kChan = 8;
     const float *ob = obj + b * C * HW;
-    float *oo = out + b * C * HW + p;
-    for (int c = 0; c < C; ++c) {
-        const float *plane = ob + int64_t(c) * HW;
-        float o[VEC];
+    float *oo = out + b * C * HW;
+    const unsigned uHW = unsigned(HW);
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) o[k] = src[k] >= 0 ? plane[src[k]] : 0.f;
-        if constexpr (VEC == 4) {
-            *reinterpret_cast<float4 *>(oo + int64_t(c) * HW) = make_float4(o[0], o[1], o[2], o[3]);
-        } else {
+    for (int s = 0; s < kSteps; ++s) {
+        const int q = threadIdx.x + s * kWarpThreads;
+        const int ly = (q * 4) / TW, lx = (q * 4) - ly * TW;
+        const int ty = y0 + ly, tx = x0 + lx;
+        if (ty >= H || tx >= W) continue;
+        const bool full = vec_ok && tx + 3 < W;
+        const unsigned t0 = unsigned(ty) * unsigned(W) + unsigned(tx);
+        const ulonglong2 k01 = *reinterpret_cast<const ulonglong2 *>(&L.zk[ly * TW + lx]);
+        const ulonglong2 k23 = *reinterpret_cast<const ulonglong2 *>(&L.zk[ly * TW + lx + 2]);
+        const unsigned long long key[4] = {k01.x, k01.y, k23.x, k23.y};
+        int src[4];
+        float vv[4], cc4[4];
 #pragma unroll
-            for (int k = 0; k < VEC; ++k) oo[int64_t(c) * HW + k] = o[k];
+        for (int k = 0; k < 4; ++k) {
+            const bool touched = key[k] != KEY_UNTOUCHED;
+            const bool nowin = key[k] == KEY_NOWIN;
+            vv[k] = touched ? 1.f : 0.f;
+            cc4[k] = nowin ? 1.f : 0.f;
+            src[k] = (touched && !nowin) ? int(key[k] & 0xFFFFFFFFull) : -1;
         }
-    }
-    if constexpr (VEC == 4) {
-        *reinterpret_cast<float4 *>(valid + b * HW + p) = make_float4(vv[0], vv[1], vv[2], vv[3]);
-        *reinterpret_cast<float4 *>(coll + b * HW + p) = make_float4(cc[0], cc[1], cc[2], cc[3]);
-    } else {
+        for (int c0 = 0; c0 < C; c0 += kChan) {
+            float o[kChan][4];
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) { valid[b * HW + p + k] = vv[k]; coll[b * HW + p + k] = cc[k]; }
+            for (int cc = 0; cc < kChan; ++cc) {
+                const bool chan = c0 + cc < C;
+                const unsigned pl = unsigned(c0 + cc) * uHW;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) o[cc][k] = (chan && src[k] >= 0) ? ob[pl + unsigned(src[k])] : 0.f;
+            }
+#pragma unroll
+            for (int cc = 0; cc < kChan; ++cc) {
+                if (c0 + cc >= C) break;
+                float *dst = oo + unsigned(c0 + cc) * uHW + t0;
+                if (full) {
+                    *reinterpret_cast<float4 *>(dst) = make_float4(o[cc][0], o[cc][1], o[cc][2], o[cc][3]);
+                } else {
+                    for (int k = 0; k < 4 && tx + k < W; ++k) dst[k] = o[cc][k];
+                }
+            }
+        }
+        float *vd = valid + b * HW + t0;
+        float *cd = coll + b * HW + t0;
+        if (full) {
+            *reinterpret_cast<float4 *>(vd) = make_float4(vv[0], vv[1], vv[2], vv[3]);
+            *reinterpret_cast<float4 *>(cd) = make_float4(cc4[0], cc4[1], cc4[2], cc4[3]);
+        } else {
+            for (int k = 0; k < 4 && tx + k < W; ++k) { vd[k] = vv[k]; cd[k] = cc4[k]; }
+        }
     }
 }
 
-// ---------------------------------------------------------------- f64 op
+// The fused launch.  Workgroup id -> (XCD-aware) slot x; slots are dealt to
+// the BIN role at an even stride among the TILE slots.  Dispatch is round-robin
+// over the 8 XCDs (workgroups b and b+8 share one), so slot x = contiguous runs
+// per XCD keeps neighbouring tiles -- which share source blocks and gather
+// rows -- in one L2.  Placement only affects speed, never results.
+template <typename Coords>
+__global__ __launch_bounds__(kWarpThreads, 4) void warp_kernel(Coords co, const float *__restrict__ obj,
+                                                               const float *__restrict__ depth,
+                                                               float *__restrict__ out, float *__restrict__ valid,
+                                                               float *__restrict__ coll, ChunkArgs tile_a,
+                                                               ChunkArgs bin_a, int C, int H, int W, int64_t HW,
+                                                               TileGeom g, int vec_ok) {
+    __shared__ WarpLds lds;
+    const unsigned N = unsigned(tile_a.nwg + bin_a.nwg);
+    const unsigned per = (N + 7u) / 8u;
+    const unsigned x = (blockIdx.x % 8u) * per + blockIdx.x / 8u;
+    if (x >= N) return;
+    // number of BIN slots among [0, x) at an even stride
+    const unsigned nb0 = unsigned((uint64_t(x) * unsigned(bin_a.nwg)) / N);
+    const unsigned nb1 = unsigned((uint64_t(x + 1) * unsigned(bin_a.nwg)) / N);
+    if (nb1 > nb0) {
+        bin_role<Coords>(lds.bin, int(nb0), co, depth, bin_a, H, W, HW, g);
+    } else {
+        tile_role<Coords>(lds.tile, int(x - nb0), co, obj, depth, out, valid, coll, tile_a, C, H, W, HW, g,
+                          vec_ok);
+    }
+}
+
+// ---------------------------------------------------------------- ATOMIC engine
+// Lane-strided: a wave covers 64*4 consecutive chunk pixels, lane l takes
+// pixels l, l+64, l+128, l+192, so every atomic / load / store wave-instruction
+// touches one contiguous span (thread-contiguous spans measured 3.5x slower
+// for 64-bit atomics, tools/microbench.hip).
+template <typename Coords>
+__global__ __launch_bounds__(kBlock) void splat_atomic_kernel(Coords co, const float *__restrict__ depth,
+                                                              unsigned long long *__restrict__ keys, int H, int W,
+                                                              int64_t HW, int64_t b0, int64_t chunk_px) {
+    const int64_t base = (int64_t(blockIdx.x) * kBlock + (threadIdx.x & ~63)) * 4 + lane_id();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int64_t q = base + k * 64;
+        int t = -1;
+        unsigned long long key = 0;
+        if (q < chunk_px) {
+            const int64_t bl = q / HW, p = q - bl * HW, b = b0 + bl;
+            const int j = int(p / W), i = int(p - int64_t(j) * W);
+            typename Coords::V x, y;
+            co.load(b, p, x, y);
+            int tx, ty;
+            co.target(i, j, x, y, H, W, tx, ty);
+            if (tx >= 0) {
+                t = int(bl * HW) + ty * W + tx;  // chunk-local slot (chunk_px < 2^31)
+                key = make_key(depth[b * HW + p], unsigned(p));
+            }
+        }
+        wave_run_atomic_min(keys, t, key);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void resolve_atomic_kernel(const float *__restrict__ obj,
+                                                                unsigned long long *__restrict__ keys,
+                                                                float *__restrict__ out, float *__restrict__ valid,
+                                                                float *__restrict__ coll, int C, int64_t HW,
+                                                                int64_t b0, int64_t chunk_px) {
+    const int64_t base = (int64_t(blockIdx.x) * kBlock + (threadIdx.x & ~63)) * 4 + lane_id();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int64_t q = base + k * 64;
+        if (q >= chunk_px) break;
+        const int64_t bl = q / HW, p = q - bl * HW, b = b0 + bl;
+        const unsigned long long key = keys[q];
+        keys[q] = KEY_UNTOUCHED;
+        const bool touched = key != KEY_UNTOUCHED;
+        const bool win = touched && key != KEY_NOWIN;
+        const int64_t s = int64_t(key & 0xFFFFFFFFull);
+        valid[b * HW + p] = touched ? 1.f : 0.f;
+        coll[b * HW + p] = (touched && !win) ? 1.f : 0.f;
+        const float *ob = obj + b * C * HW;
+        float *oo = out + b * C * HW + p;
+        for (int c = 0; c < C; ++c) oo[int64_t(c) * HW] = win ? ob[int64_t(c) * HW + s] : 0.f;
+    }
+}
+
+// ---------------------------------------------------------------- f64 op (atomic)
 // Exact double depths do not fit a 32-bit key half, so the double path keys
 // on the full 64-bit orderable depth first, then resolves ties by a 32-bit
 // index min among the sources that hold the minimum depth.
@@ -259,11 +632,12 @@ __global__ __launch_bounds__(kBlock) void splat_f64_depth_kernel(
     const int64_t q = int64_t(blockIdx.x) * kBlock + threadIdx.x;
     if (q >= chunk_px) return;
     const int64_t g = b0 * HW + q;
-    const int t = target_safe<double>(sx[g], sy[g], H, W);
-    if (t < 0) return;
+    int tx, ty;
+    target_safe<double>(sx[g], sy[g], H, W, tx, ty);
+    if (tx < 0) return;
     const double d = depth[g];
     const unsigned long long z = (d < 1000.0) ? orderable64(d) : ZKEY_NOWIN;
-    atomicMin(zkeys + (q / HW) * HW + t, z);
+    atomicMin(zkeys + (q / HW) * HW + int64_t(ty) * W + tx, z);
 }
 
 __global__ __launch_bounds__(kBlock) void splat_f64_index_kernel(
@@ -275,9 +649,10 @@ __global__ __launch_bounds__(kBlock) void splat_f64_index_kernel(
     const int64_t g = b0 * HW + q;
     const double d = depth[g];
     if (!(d < 1000.0)) return;
-    const int t = target_safe<double>(sx[g], sy[g], H, W);
-    if (t < 0) return;
-    const int64_t slot = (q / HW) * HW + t;
+    int tx, ty;
+    target_safe<double>(sx[g], sy[g], H, W, tx, ty);
+    if (tx < 0) return;
+    const int64_t slot = (q / HW) * HW + int64_t(ty) * W + tx;
     if (zkeys[slot] == orderable64(d)) atomicMin(idx + slot, (unsigned int)(q % HW));
 }
 
@@ -302,8 +677,8 @@ __global__ __launch_bounds__(kBlock) void resolve_f64_kernel(
 }
 
 // ---------------------------------------------------------------- host side
-inline unsigned grid_for(int64_t work_items) {
-    return unsigned((work_items + kBlock - 1) / kBlock);
+inline unsigned grid_for(int64_t work_items, int per_block = kBlock) {
+    return unsigned((work_items + per_block - 1) / per_block);
 }
 
 inline bool aligned(const void *p, size_t a) { return (reinterpret_cast<uintptr_t>(p) % a) == 0; }
@@ -314,38 +689,98 @@ int check_dims(int64_t B, int64_t C, int64_t H, int64_t W) {
     return OFD_FW_OK;
 }
 
-// images per chunk for a workspace of `bytes` (per-image slab `per_image`)
-int64_t chunk_images(int64_t B, int64_t per_image, size_t bytes) {
-    int64_t g = int64_t(bytes / size_t(per_image));
+enum class Mode { Tile = 0, Atomic = 1 };
+
+// Engine selection: OFD_FW_MODE=atomic in the environment, or
+// ofd_fw_set_engine() at run time (tests and benchmarks compare the two).
+int g_engine = -1;
+
+Mode engine_mode() {
+    if (g_engine < 0) {
+        const char *e = getenv("OFD_FW_MODE");
+        g_engine = (e && strcmp(e, "atomic") == 0) ? int(Mode::Atomic) : int(Mode::Tile);
+    }
+    return Mode(g_engine);
+}
+
+// images per chunk for a workspace of `bytes`; chunk pixels stay < 2^31
+int64_t chunk_images(int64_t B, int64_t HW, size_t per_image, size_t bytes) {
+    int64_t g = int64_t(bytes / per_image);
+    const int64_t cap = ((int64_t(1) << 31) - 1) / HW;
+    if (g > cap) g = cap;
     return g < B ? g : B;
 }
 
+// C == 0: the reference launches no channel-0 thread, so valid and collision
+// stay as allocated, all zero (fw_cuda_kernel.cu:59-60, :38).
+int zero_masks(void *valid, void *coll, size_t bytes, hipStream_t st) {
+    hipError_t e = hipMemsetAsync(valid, 0, bytes, st);
+    if (e == hipSuccess) e = hipMemsetAsync(coll, 0, bytes, st);
+    return e == hipSuccess ? OFD_FW_OK : int(e);
+}
+
 template <typename Coords>
-int run_f32(Coords co, bool coords_vec_ok, const float *obj, const float *depth, float *out, float *valid,
-            float *coll, int64_t B, int64_t C, int64_t H, int64_t W, void *ws, size_t ws_bytes,
-            hipStream_t st) {
+int run_f32(Coords co, const float *obj, const float *depth, float *out, float *valid, float *coll,
+            int64_t B, int64_t C, int64_t H, int64_t W, void *ws, size_t ws_bytes, hipStream_t st) {
     const int64_t HW = H * W;
     if (B == 0 || HW == 0) return OFD_FW_OK;
-    const int64_t per_image = HW * int64_t(sizeof(unsigned long long));
+    if (C == 0) return zero_masks(valid, coll, size_t(B * HW) * sizeof(float), st);
     if (!ws || !aligned(ws, 16)) return OFD_FW_EWORKSPACE;
-    const int64_t G = chunk_images(B, per_image, ws_bytes);
-    if (G < 1) return OFD_FW_EWORKSPACE;
-    auto *keys = static_cast<unsigned long long *>(ws);
-    const bool vec = (HW % 4 == 0) && coords_vec_ok && aligned(depth, 16) && aligned(obj, 4) &&
-                     aligned(out, 16) && aligned(valid, 16) && aligned(coll, 16);
-    for (int64_t b0 = 0; b0 < B; b0 += G) {
-        const int64_t nb = (B - b0) < G ? (B - b0) : G;
-        const int64_t px = nb * HW;
-        if (vec) {
-            hipLaunchKernelGGL((splat_f32_kernel<4, Coords>), dim3(grid_for(px / 4)), dim3(kBlock), 0, st,
+    const size_t per_image = per_image_bytes(H, W);
+    const TileGeom g = make_geom(H, W);
+    const int vec_ok = (W % 4 == 0) && aligned(out, 16) && aligned(valid, 16) && aligned(coll, 16);
+    // the tile engine's gathers use 32-bit offsets inside one image
+    const Mode mode = (C * HW < (int64_t(1) << 30)) ? engine_mode() : Mode::Atomic;
+
+    if (mode == Mode::Atomic) {
+        const int64_t G = chunk_images(B, HW, per_image, ws_bytes);
+        if (G < 1) return OFD_FW_EWORKSPACE;
+        auto *keys = static_cast<unsigned long long *>(ws);
+        for (int64_t b0 = 0; b0 < B; b0 += G) {
+            const int64_t nb = (B - b0) < G ? (B - b0) : G;
+            const int64_t px = nb * HW;
+            hipLaunchKernelGGL((splat_atomic_kernel<Coords>), dim3(grid_for(px, kBlock * 4)), dim3(kBlock), 0, st,
                                co, depth, keys, int(H), int(W), HW, b0, px);
-            hipLaunchKernelGGL((resolve_f32_kernel<4>), dim3(grid_for(px / 4)), dim3(kBlock), 0, st,
+            hipLaunchKernelGGL(resolve_atomic_kernel, dim3(grid_for(px, kBlock * 4)), dim3(kBlock), 0, st,
                                obj, keys, out, valid, coll, int(C), HW, b0, px);
+        }
+    } else {
+        // Two slabs when they fit: chunk c uses slab c % 2, and launch L runs
+        // TILE(chunk L-1) beside BIN(chunk L).  One slab: BIN and TILE launches
+        // alternate.
+        int64_t G = chunk_images(B, HW, per_image, ws_bytes / 2);
+        int nslab = 2;
+        if (G < 1 || G >= B) {
+            G = chunk_images(B, HW, per_image, ws_bytes);
+            nslab = 1;
+        }
+        if (G < 1) return OFD_FW_EWORKSPACE;
+        const int64_t nch = (B + G - 1) / G;
+        Ws slab[2];
+        slab[0] = carve(ws, G, HW, g);
+        slab[1] = carve(static_cast<char *>(ws) + size_t(G) * per_image, G, HW, g);
+        auto chunk = [&](int64_t c, int role_bin) {
+            ChunkArgs a;
+            a.ws = slab[nslab == 2 ? c % 2 : 0];
+            a.b0 = c * G;
+            a.nimg = int((B - a.b0) < G ? (B - a.b0) : G);
+            a.nwg = role_bin ? int((int64_t(a.nimg) * g.nsb + kBinBlocks - 1) / kBinBlocks) : a.nimg * g.ntiles;
+            return a;
+        };
+        ChunkArgs none{};
+        auto launch = [&](const ChunkArgs &t, const ChunkArgs &b) {
+            const unsigned N = unsigned(t.nwg + b.nwg);
+            hipLaunchKernelGGL((warp_kernel<Coords>), dim3((N + 7u) / 8u * 8u), dim3(kWarpThreads), 0, st,
+                               co, obj, depth, out, valid, coll, t, b, int(C), int(H), int(W), HW, g, vec_ok);
+        };
+        if (nslab == 2) {
+            for (int64_t L = 0; L <= nch; ++L)
+                launch(L >= 1 ? chunk(L - 1, 0) : none, L < nch ? chunk(L, 1) : none);
         } else {
-            hipLaunchKernelGGL((splat_f32_kernel<1, Coords>), dim3(grid_for(px)), dim3(kBlock), 0, st,
-                               co, depth, keys, int(H), int(W), HW, b0, px);
-            hipLaunchKernelGGL((resolve_f32_kernel<1>), dim3(grid_for(px)), dim3(kBlock), 0, st,
-                               obj, keys, out, valid, coll, int(C), HW, b0, px);
+            for (int64_t c = 0; c < nch; ++c) {
+                launch(none, chunk(c, 1));
+                launch(chunk(c, 0), none);
+            }
         }
     }
     const hipError_t e = hipGetLastError();
@@ -358,12 +793,18 @@ extern "C" {
 
 int ofd_fw_abi_version(void) { return OFD_FW_ABI_VERSION; }
 
+int ofd_fw_set_engine(int engine) {
+    const int prev = int(engine_mode());
+    if (engine == OFD_FW_ENGINE_TILE || engine == OFD_FW_ENGINE_ATOMIC) g_engine = engine;
+    return prev;
+}
+
 const char *ofd_fw_strerror(int code) {
     switch (code) {
         case OFD_FW_OK: return "success";
         case OFD_FW_EINVAL: return "invalid argument (null pointer or negative dimension)";
         case OFD_FW_ETOOBIG: return "H*W must be < 2^31";
-        case OFD_FW_EWORKSPACE: return "workspace missing, misaligned or smaller than one image's key slab";
+        case OFD_FW_EWORKSPACE: return "workspace missing, misaligned or smaller than one image's slab";
         case OFD_FW_EALIGN: return "pointer misaligned for its dtype";
         default: return code > 0 ? hipGetErrorString(hipError_t(code)) : "unknown error";
     }
@@ -371,12 +812,15 @@ const char *ofd_fw_strerror(int code) {
 
 size_t ofd_fw_workspace_bytes(int64_t B, int64_t H, int64_t W, int f64) {
     if (B <= 0 || H <= 0 || W <= 0) return 0;
-    const size_t per_image = size_t(H) * size_t(W) * (f64 ? (sizeof(unsigned long long) + sizeof(unsigned int))
-                                                           : sizeof(unsigned long long));
-    size_t g = kDefaultSlabBytes / per_image;
+    if (f64) return size_t(B < 8 ? B : 8) * size_t(H) * size_t(W) * (sizeof(unsigned long long) + sizeof(unsigned int));
+    const size_t per_image = per_image_bytes(H, W);
+    // chunk = the images whose slabs and re-read planes stay cache-resident
+    // between a chunk's BIN and TILE roles; OFD_FW_CHUNK_IMAGES overrides.
+    size_t g = kDefaultChunkBytes / per_image;
+    if (const char *e = getenv("OFD_FW_CHUNK_IMAGES")) g = size_t(atoi(e));
     if (g < 1) g = 1;
-    if (g > size_t(B)) g = size_t(B);
-    return g * per_image;
+    if (g >= size_t(B)) return size_t(B) * per_image;  // one chunk, one slab
+    return 2 * g * per_image;                          // double-buffered slabs
 }
 
 int ofd_fw_workspace_init(void *workspace, size_t bytes, void *stream) {
@@ -394,8 +838,7 @@ int ofd_fw_forward_warping_f32(const float *obj, const float *safe_y, const floa
     if (B * H * W > 0 && (!safe_y || !safe_x || !depth || !valid || !collision || (C > 0 && (!obj || !output))))
         return OFD_FW_EINVAL;
     SafeF32 co{safe_y, safe_x, H * W};
-    const bool vec_ok = aligned(safe_y, 16) && aligned(safe_x, 16);
-    return run_f32(co, vec_ok, obj, depth, output, valid, collision, B, C, H, W, workspace, workspace_bytes,
+    return run_f32(co, obj, depth, output, valid, collision, B, C, H, W, workspace, workspace_bytes,
                    static_cast<hipStream_t>(stream));
 }
 
@@ -406,8 +849,8 @@ int ofd_fw_forward_warp_flow_f32(const float *obj, const float *flow, const floa
     if (B * H * W > 0 && (!flow || !depth || !valid || !collision || (C > 0 && (!obj || !output))))
         return OFD_FW_EINVAL;
     FlowCoords<float> co{flow, H * W};
-    return run_f32(co, aligned(flow, 16), obj, depth, output, valid, collision, B, C, H, W, workspace,
-                   workspace_bytes, static_cast<hipStream_t>(stream));
+    return run_f32(co, obj, depth, output, valid, collision, B, C, H, W, workspace, workspace_bytes,
+                   static_cast<hipStream_t>(stream));
 }
 
 int ofd_fw_forward_warp_flow_f64flow(const float *obj, const double *flow, const float *depth, float *output,
@@ -418,7 +861,7 @@ int ofd_fw_forward_warp_flow_f64flow(const float *obj, const double *flow, const
         return OFD_FW_EINVAL;
     if (!aligned(flow, 8)) return OFD_FW_EALIGN;
     FlowCoords<double> co{flow, H * W};
-    return run_f32(co, aligned(flow, 16), obj, depth, output, valid, collision, B, C, H, W, workspace, workspace_bytes,
+    return run_f32(co, obj, depth, output, valid, collision, B, C, H, W, workspace, workspace_bytes,
                    static_cast<hipStream_t>(stream));
 }
 
@@ -431,13 +874,14 @@ int ofd_fw_forward_warping_f64(const double *obj, const double *safe_y, const do
     if (B == 0 || HW == 0) return OFD_FW_OK;
     if (!safe_y || !safe_x || !depth || !valid || !collision || (C > 0 && (!obj || !output)))
         return OFD_FW_EINVAL;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (C == 0) return zero_masks(valid, collision, size_t(B * HW) * sizeof(double), st);
     if (!workspace || !aligned(workspace, 16)) return OFD_FW_EWORKSPACE;
-    const int64_t per_image = HW * int64_t(sizeof(unsigned long long) + sizeof(unsigned int));
-    const int64_t G = chunk_images(B, per_image, workspace_bytes);
+    const size_t per_image = size_t(HW) * (sizeof(unsigned long long) + sizeof(unsigned int));
+    const int64_t G = chunk_images(B, HW, per_image, workspace_bytes);
     if (G < 1) return OFD_FW_EWORKSPACE;
     auto *zkeys = static_cast<unsigned long long *>(workspace);
     auto *idx = reinterpret_cast<unsigned int *>(zkeys + G * HW);
-    hipStream_t st = static_cast<hipStream_t>(stream);
     for (int64_t b0 = 0; b0 < B; b0 += G) {
         const int64_t nb = (B - b0) < G ? (B - b0) : G;
         const int64_t px = nb * HW;

@@ -174,8 +174,9 @@ def test_chunked_workspace_via_c_abi(cuda_device):
     obj, flow, depth = synth.stage_one_batch(list(range(B)), H, W, cuda_device)
     exp = oracle.fw_flow(obj.cpu().numpy(), flow.cpu().numpy(), depth.cpu().numpy())
     stream = torch.cuda.current_stream(cuda_device).cuda_stream
+    one = lib.ofd_fw_workspace_bytes(1, H, W, 0)
     for images_per_chunk in (1, 2, 3, 7):
-        nbytes = images_per_chunk * H * W * 8
+        nbytes = images_per_chunk * one
         ws = torch.empty(nbytes, dtype=torch.uint8, device=cuda_device)
         assert lib.ofd_fw_workspace_init(ws.data_ptr(), nbytes, stream) == 0
         out = torch.empty_like(obj)
@@ -250,3 +251,56 @@ def test_FW_3d_matches_batched(cuda_device):
         o, v, c = fw(obj[i], flow[i], depth[i])
         assert o.shape == (6, 40, 56) and v.shape == (1, 40, 56) and c.shape == (1, 40, 56)
         assert torch.equal(o, ob[i]) and torch.equal(v, vb[i]) and torch.equal(c, cb[i])
+
+
+# ------------------------------------------------------------------ both engines
+@pytest.fixture
+def atomic_engine():
+    from opticalflowfromdepth_amd import _native
+    lib = _native.lib()
+    prev = lib.ofd_fw_set_engine(1)
+    yield
+    lib.ofd_fw_set_engine(prev)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_atomic_engine_random_vs_oracle(cuda_device, atomic_engine, seed):
+    from opticalflowfromdepth_amd import forward_warp_flow
+    rng = np.random.default_rng(100 + seed)
+    B, C, H, W = 3, int(rng.choice([2, 6, 7])), int(rng.integers(5, 90)), int(rng.integers(5, 120))
+    obj = rng.standard_normal((B, C, H, W)).astype(np.float32)
+    flow = (rng.standard_normal((B, 2, H, W)) * rng.uniform(0.1, 60)).astype(np.float32)
+    depth = rng.integers(0, 4, (B, 1, H, W)).astype(np.float32)
+    got = forward_warp_flow(_t(obj, cuda_device), _t(flow, cuda_device), _t(depth, cuda_device))
+    _assert_same(got, oracle.fw_flow(obj, flow, depth), f"atomic seed{seed}")
+
+
+def test_engines_agree_on_realistic_batch(cuda_device):
+    from opticalflowfromdepth_amd import _native, forward_warp_flow, synth
+    lib = _native.lib()
+    obj, flow, depth = synth.stage_one_batch([12345 + i for i in range(8)], 384, 512, cuda_device)
+    prev = lib.ofd_fw_set_engine(0)
+    try:
+        a = forward_warp_flow(obj, flow, depth)
+        lib.ofd_fw_set_engine(1)
+        b = forward_warp_flow(obj, flow, depth)
+    finally:
+        lib.ofd_fw_set_engine(prev)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+
+
+def test_tile_engine_overflow_and_wide_boxes(cuda_device):
+    """Border hot spots overflow tile lists; random flows give boxes wider than
+    the tile budget.  Both spill to the key slab and must stay bit-exact."""
+    from opticalflowfromdepth_amd import forward_warp_flow
+    rng = np.random.default_rng(21)
+    B, C, H, W = 2, 6, 256, 384
+    obj = rng.standard_normal((B, C, H, W)).astype(np.float32)
+    flow = np.zeros((B, 2, H, W), np.float32)
+    flow[0, 0] = 5000.0                                       # every source -> column W-1 (overflow)
+    flow[0, 1] = (rng.standard_normal((H, W)) * 3).astype(np.float32)
+    flow[1] = (rng.standard_normal((2, H, W)) * 150).astype(np.float32)   # non-smooth
+    depth = rng.integers(1, 5, (B, 1, H, W)).astype(np.float32)
+    got = forward_warp_flow(_t(obj, cuda_device), _t(flow, cuda_device), _t(depth, cuda_device))
+    _assert_same(got, oracle.fw_flow(obj, flow, depth), "overflow")

@@ -43,11 +43,22 @@ def test_workspace_bytes():
     from opticalflowfromdepth_amd import _native
     lib = _native.lib()
     hw = 768 * 1024
+    one = lib.ofd_fw_workspace_bytes(1, 768, 1024, 0)
+    assert one >= hw * 8  # key slab + tile lists
     b = lib.ofd_fw_workspace_bytes(64, 768, 1024, 0)
-    assert b % (hw * 8) == 0 and 1 <= b // (hw * 8) <= 64
-    assert lib.ofd_fw_workspace_bytes(1, 768, 1024, 0) == hw * 8
+    assert b % one == 0 and 1 <= b // one <= 64
     assert lib.ofd_fw_workspace_bytes(2, 4, 4, 1) == 2 * 16 * 12
     assert lib.ofd_fw_workspace_bytes(0, 4, 4, 0) == 0
+
+
+def test_engine_switch():
+    from opticalflowfromdepth_amd import _native
+    lib = _native.lib()
+    cur = lib.ofd_fw_set_engine(-1)
+    assert cur in (0, 1)
+    assert lib.ofd_fw_set_engine(1) == cur
+    assert lib.ofd_fw_set_engine(0) == 1
+    lib.ofd_fw_set_engine(cur)
 
 
 def test_argument_errors_without_gpu():

@@ -1,0 +1,85 @@
+// tools/microbench.hip -- design probes for the forward-warp engine (gfx950).
+// Measures: HBM stream-copy ceiling; global 64-bit atomicMin throughput by
+// access shape and footprint; 32-bit atomicMin; LDS 64-bit atomicMin.
+// Build: hipcc --offload-arch=gfx950 -O3 -o tools/microbench tools/microbench.hip
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
+
+__global__ void copy4(const float4* __restrict__ a, float4* __restrict__ b, size_t n) {
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    size_t st = (size_t)gridDim.x * blockDim.x;
+    for (; i < n; i += st) b[i] = a[i];
+}
+
+// each thread: VEC atomics; shape 0 = lane-contiguous per instruction (addr = base + k*64 + lane)
+// shape 1 = thread-contiguous (addr = base + lane*VEC + k)  (v1 kernel's shape)
+template <int SHAPE, typename T>
+__global__ void atom(T* __restrict__ buf, size_t n_atomics, size_t mask, unsigned salt) {
+    const int VEC = 4;
+    size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    size_t wave = t / 64, lane = t % 64;
+    size_t base = wave * 64 * VEC;
+    if (base >= n_atomics) return;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+        size_t idx = SHAPE == 0 ? base + k * 64 + lane : base + lane * VEC + k;
+        atomicMin(buf + (idx & mask), (T)(idx ^ salt));
+    }
+}
+
+__global__ void lds_atom(unsigned long long* out, int iters) {
+    __shared__ unsigned long long z[4096];
+    for (int i = threadIdx.x; i < 4096; i += blockDim.x) z[i] = ~0ull;
+    __syncthreads();
+    unsigned long long v = blockIdx.x * 7919ull + threadIdx.x;
+    for (int it = 0; it < iters; ++it) {
+        int a = (threadIdx.x * 13 + it * 64) & 4095;
+        atomicMin(&z[a], v ^ (unsigned long long)it);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) out[blockIdx.x] = z[blockIdx.x & 4095];
+}
+
+template <typename F>
+float timeit(F f, int reps = 10) {
+    hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+    f(); CK(hipDeviceSynchronize());
+    CK(hipEventRecord(a));
+    for (int r = 0; r < reps; ++r) f();
+    CK(hipEventRecord(b)); CK(hipEventSynchronize(b));
+    float ms; CK(hipEventElapsedTime(&ms, a, b));
+    return ms / reps;
+}
+
+int main() {
+    const size_t n4 = (size_t)1 << 28;  // 4 GiB as float4? no: 2^28 float4 = 4 GiB; use 2^26 = 1 GiB
+    size_t n = (size_t)1 << 26;
+    float4 *a, *b; CK(hipMalloc(&a, n * 16)); CK(hipMalloc(&b, n * 16));
+    CK(hipMemset(a, 0, n * 16));
+    float ms = timeit([&] { copy4<<<2048 * 4, 256>>>(a, b, n); });
+    printf("copy float4 1GiB->1GiB: %.3f ms  %.1f GB/s (read+write)\n", ms, 2.0 * n * 16 / ms / 1e6);
+    (void)n4;
+
+    const size_t NA = 50331648;  // one headline step of sources
+    unsigned long long* keys; CK(hipMalloc(&keys, ((size_t)1 << 26) * 8));
+    unsigned* k32; CK(hipMalloc(&k32, ((size_t)1 << 26) * 4));
+    const size_t blocks = (NA / 4 + 255) / 256;
+    for (size_t lg : {26, 23, 19}) {
+        size_t mask = ((size_t)1 << lg) - 1;
+        CK(hipMemset(keys, 0xFF, ((size_t)1 << 26) * 8));
+        float m0 = timeit([&] { atom<0, unsigned long long><<<blocks, 256>>>(keys, NA, mask, 12345u); });
+        float m1 = timeit([&] { atom<1, unsigned long long><<<blocks, 256>>>(keys, NA, mask, 12345u); });
+        float m2 = timeit([&] { atom<0, unsigned><<<blocks, 256>>>(k32, NA, mask, 12345u); });
+        printf("footprint %zu slots: u64 lane-contig %.3f ms (%.1f Gatom/s)  u64 thread-contig %.3f ms (%.1f)  u32 lane-contig %.3f ms (%.1f)\n",
+               mask + 1, m0, NA / m0 / 1e6, m1, NA / m1 / 1e6, m2, NA / m2 / 1e6);
+    }
+    unsigned long long* o; CK(hipMalloc(&o, 1 << 20));
+    int iters = 4096;
+    float ml = timeit([&] { lds_atom<<<2048, 256>>>(o, iters); });
+    printf("LDS u64 atomicMin: %.3f ms  %.1f Gatom/s chip\n", ml, 2048.0 * 256 * iters / ml / 1e6);
+    return 0;
+}
