@@ -71,13 +71,17 @@ int ofd_fw_set_engine(int engine);
 /* Human-readable name of a return code (static storage). */
 const char *ofd_fw_strerror(int code);
 
-/* Bytes of key workspace a call with these sizes needs.  f64 != 0 for the
- * float64 op.  The workspace is reused across calls and must be initialised
- * once with ofd_fw_workspace_init(); every successful call leaves it
- * initialised again. */
+/* Bytes of workspace recommended for a call with these sizes (f64 != 0 for
+ * the float64 op); any size of at least one image's share works, larger
+ * workspaces process more images per chunk.  The workspace is reused across
+ * calls: initialise it once with ofd_fw_workspace_init(); every successful
+ * call leaves the parts that must start initialised (key slabs, tile flags)
+ * in that state again.  Calls sharing a workspace must be stream-ordered. */
 size_t ofd_fw_workspace_bytes(int64_t B, int64_t H, int64_t W, int f64);
 
-/* Put `bytes` of workspace into its initial state (async on `stream`). */
+/* Put `bytes` of workspace into its initial state (async on `stream`).  Call
+ * it for every new workspace allocation (the library remembers, per workspace
+ * address, which layout last used it, and re-initialises on a layout change). */
 int ofd_fw_workspace_init(void *workspace, size_t bytes, void *stream);
 
 /* fw_cuda.forward_warping, float32.  obj/output [B,C,H,W]; safe_y, safe_x,

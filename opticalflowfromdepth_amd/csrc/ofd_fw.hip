@@ -34,9 +34,10 @@
 //  ATOMIC (OFD_FW_MODE=atomic; and the float64 op).  One global 64-bit atomic
 //  min per source into a per-image key slab, then a resolve pass.
 //
-// Workspace invariant: every call leaves the caller's workspace bytes all-ones
-// (keys = KEY_UNTOUCHED, tile counters encoded as ~count, flags ~0), so the
-// workspace is initialised once (ofd_fw_workspace_init) and never cleared.
+// Workspace invariant: every call leaves the key slabs and tile flags all-ones
+// (keys = KEY_UNTOUCHED, flags ~0), so the workspace is initialised once
+// (ofd_fw_workspace_init) and never cleared; the per-block target boxes are
+// scratch rewritten by every call.
 //
 // Plain HIP for gfx950; no CUDA compatibility layer, no dual paths.
 
@@ -45,6 +46,9 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+
+#include <mutex>
+#include <unordered_map>
 
 #include "ofd_fw.h"
 
@@ -60,7 +64,7 @@ constexpr unsigned int IDX_NONE = ~0u;
 // tile engine geometry
 constexpr int TW = 128, TH = 32;          // target tile (LDS z-buffer 32 KiB)
 constexpr int SBW = 16, SBH = 4;          // source block = one wave (64 px)
-constexpr int CAP = 256;                  // list entries per tile before overflow
+constexpr int SEGB = 8;                   // source blocks per segment (128 x 4 px)
 constexpr int MAX_TILES_PER_BLOCK = 12;   // wider boxes go through the global path
 constexpr int kUnroll = 4;                // source pixels in flight per thread
 
@@ -147,16 +151,23 @@ struct FlowCoords {  // FW.forward input: flow [B,2,H,W], ch0 = x, ch1 = y
 // ---------------------------------------------------------------- wave helpers
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
-__device__ __forceinline__ int wave_min(int v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) { const int o = __shfl_xor(v, d); v = o < v ? o : v; }
-    return v;
+// Wave-wide min / max with DPP row operations (no LDS round trip): quad
+// swaps, row mirrors, then the row_bcast:15 / row_bcast:31 steps fold the four
+// 16-lane rows into lane 63, which readlane broadcasts.
+template <bool kMin>
+__device__ __forceinline__ int wave_reduce(int v) {
+    constexpr int ident = kMin ? 0x7FFFFFFF : int(0x80000000);
+    auto op = [](int a, int b) { return kMin ? (a < b ? a : b) : (a > b ? a : b); };
+    v = op(v, __builtin_amdgcn_update_dpp(ident, v, 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+    v = op(v, __builtin_amdgcn_update_dpp(ident, v, 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+    v = op(v, __builtin_amdgcn_update_dpp(ident, v, 0x141, 0xF, 0xF, false));  // row_half_mirror
+    v = op(v, __builtin_amdgcn_update_dpp(ident, v, 0x140, 0xF, 0xF, false));  // row_mirror
+    v = op(v, __builtin_amdgcn_update_dpp(ident, v, 0x142, 0xA, 0xF, false));  // row_bcast:15
+    v = op(v, __builtin_amdgcn_update_dpp(ident, v, 0x143, 0xC, 0xF, false));  // row_bcast:31
+    return __builtin_amdgcn_readlane(v, 63);
 }
-__device__ __forceinline__ int wave_max(int v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) { const int o = __shfl_xor(v, d); v = o > v ? o : v; }
-    return v;
-}
+__device__ __forceinline__ int wave_min(int v) { return wave_reduce<true>(v); }
+__device__ __forceinline__ int wave_max(int v) { return wave_reduce<false>(v); }
 
 // Global atomic min of `key` into base[t] for every lane with t >= 0, issuing
 // one atomic per run of consecutive lanes with the same t (border clamping
@@ -188,6 +199,7 @@ __device__ __forceinline__ void wave_run_atomic_min(unsigned long long *base, in
 struct TileGeom {
     int tilesX, tilesY, ntiles;  // target tiles per image
     int nsbx, nsby, nsb;         // source blocks per image
+    int nsegx, nseg;             // segments (SEGB blocks of one block row) per image
 };
 
 inline TileGeom make_geom(int64_t H, int64_t W) {
@@ -198,63 +210,76 @@ inline TileGeom make_geom(int64_t H, int64_t W) {
     g.nsbx = int((W + SBW - 1) / SBW);
     g.nsby = int((H + SBH - 1) / SBH);
     g.nsb = g.nsbx * g.nsby;
+    g.nsegx = (g.nsbx + SEGB - 1) / SEGB;
+    g.nseg = g.nsegx * g.nsby;
     return g;
 }
 
-// Per-image workspace: key slab (HW u64) + tile counters + flags + lists.
+inline size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
+
+// Per-image workspace: key slab (HW u64, only touched by spills), per-tile
+// spill flags, and the target-tile boxes of every source segment and block.
 inline size_t per_image_bytes(int64_t H, int64_t W) {
     const TileGeom g = make_geom(H, W);
-    return size_t(H) * size_t(W) * 8 + size_t(g.ntiles) * (8 + size_t(CAP) * 4);
+    return size_t(H) * size_t(W) * 8 + size_t(g.ntiles) * 4 + size_t(g.nseg) * 8 + size_t(g.nsb) * 8 + 48;
 }
 
 struct Ws {  // views of one chunk's workspace (G images)
-    unsigned long long *keys;  // [G][HW]
-    unsigned int *cnt;         // [G][ntiles], ~count
-    unsigned int *flag;        // [G][ntiles], 0 = merge key slab, ~0 = clean
-    unsigned int *list;        // [G][ntiles][CAP]
+    unsigned long long *keys;  // [G][HW]      KEY_UNTOUCHED between calls
+    unsigned int *flag;        // [G][ntiles]  0 = merge key slab, ~0 = clean
+    ushort4 *segrec;           // [G][nseg]    target tile box (t0x,t1x,t0y,t1y) of a segment
+    ushort4 *blkrec;           // [G][nsb]     same per source block
 };
 
 inline Ws carve(void *ws, int64_t G, int64_t HW, const TileGeom &g) {
     Ws w;
     char *p = static_cast<char *>(ws);
     w.keys = reinterpret_cast<unsigned long long *>(p);
-    p += size_t(G) * size_t(HW) * 8;
-    w.cnt = reinterpret_cast<unsigned int *>(p);
-    p += size_t(G) * g.ntiles * 4;
+    p += align16(size_t(G) * size_t(HW) * 8);
     w.flag = reinterpret_cast<unsigned int *>(p);
-    p += size_t(G) * g.ntiles * 4;
-    w.list = reinterpret_cast<unsigned int *>(p);
+    p += align16(size_t(G) * g.ntiles * 4);
+    w.segrec = reinterpret_cast<ushort4 *>(p);
+    p += align16(size_t(G) * g.nseg * 8);
+    w.blkrec = reinterpret_cast<ushort4 *>(p);
     return w;
+}
+
+// empty box: no t0x <= x holds
+__device__ __forceinline__ ushort4 empty_box() { return make_ushort4(0xFFFF, 0, 0xFFFF, 0); }
+__device__ __forceinline__ bool box_has(const ushort4 &r, int tx, int ty) {
+    return int(r.x) <= tx && tx <= int(r.y) && int(r.z) <= ty && ty <= int(r.w);
 }
 
 // ---------------------------------------------------------------- TILE engine
 // One fused, pipelined kernel per chunk boundary: launch L runs the TILE role
 // for chunk L-1 and the BIN role for chunk L side by side (their workspace
-// slabs alternate), so the latency-bound binning hides under the streaming
-// tile resolve.  Roles are interleaved evenly over the grid.
+// slabs alternate), roles interleaved evenly over the grid.
+//
+// BIN  : one wave per source segment (SEGB blocks of 16x4 px).  Streams the
+//        flow, writes each block's target-tile box and the segment's union box.
+//        No atomics, no lists: a pure streaming pass.  A block whose box spans
+//        more than MAX_TILES_PER_BLOCK tiles (non-smooth flow) is not boxed: its
+//        sources go to the key slab by global atomic min (pre-reduced over runs
+//        of equal targets) and flag their target tiles.
+// TILE : one workgroup per target tile.  Finds its source blocks by scanning
+//        the segment boxes of the image, then the block boxes of the selected
+//        segments (both L2-resident), folds the selected blocks' keys into an
+//        LDS z-buffer (ds_min_u64), merges the key slab if flagged, and
+//        resolves: gathers the winners' channels, writes output / valid /
+//        collision exactly once.
 constexpr int kWarpThreads = 512;
 constexpr int kWaves = kWarpThreads / 64;
-constexpr int kBinBlocks = kWaves * 4;                         // 4 source blocks per wave
-constexpr int kMaxRegs = kBinBlocks * MAX_TILES_PER_BLOCK;     // (block, tile) registrations
-
-struct BinLds {
-    int box[kBinBlocks][4];  // tile range t0x,t1x,t0y,t1y; t0x = -1 empty, -2 wide
-    int img[kBinBlocks], sb[kBinBlocks];
-    int off[kBinBlocks + 1];
-    int reg_tile[kMaxRegs];  // chunk-global tile id (image * ntiles + tile)
-    unsigned int base[kMaxRegs];
-    unsigned int slot[kMaxRegs];
-    unsigned char reg_blk[kMaxRegs];
-};
+constexpr int kSegCap = 768;    // selected segments held in LDS (else: scan all blocks)
+constexpr int kListCap = 1024;  // candidate blocks examined per batch
 
 struct TileLds {
     unsigned long long zk[TW * TH];
-    unsigned int list[CAP];
-    unsigned int n, flag;
+    unsigned int seg[kSegCap];
+    unsigned int blk[kListCap];
+    unsigned int nseg, nblk, flag;
 };
 
 union __align__(16) WarpLds {
-    BinLds bin;
     TileLds tile;
 };
 
@@ -265,203 +290,177 @@ struct ChunkArgs {  // one chunk's share of a launch
     int nwg;        // workgroups of this role in the launch
 };
 
-// ---- BIN role: kBinBlocks consecutive source blocks per workgroup.  Each
-// wave computes its blocks' target bounding boxes; the workgroup aggregates
-// the (block, tile) registrations in LDS so each distinct tile costs ONE
-// returning global atomic per workgroup (all issued together), then writes the
-// list entries.  Registrations past a tile's CAP and blocks whose box spans
-// more than MAX_TILES_PER_BLOCK tiles spill to the key slab.
+// ---- BIN role: wave w of workgroup wg boxes segment wg * kWaves + w.
 template <typename Coords>
-__device__ __forceinline__ void bin_role(BinLds &L, int wg, const Coords &co, const float *__restrict__ depth,
+__device__ __forceinline__ void bin_role(int wg, const Coords &co, const float *__restrict__ depth,
                                          const ChunkArgs &a, int H, int W, int64_t HW, const TileGeom &g) {
     const Ws &ws = a.ws;
-    const int lane = lane_id(), wave = threadIdx.x >> 6;
-    const int64_t nblk = int64_t(a.nimg) * g.nsb;
-    int tx[4], ty[4];
+    const int lane = lane_id();
+    const int64_t sgg = int64_t(wg) * kWaves + (threadIdx.x >> 6);
+    if (sgg >= int64_t(a.nimg) * g.nseg) return;  // wave-uniform
+    const int bl = int(sgg / g.nseg);
+    const int sg = int(sgg - int64_t(bl) * g.nseg);
+    const int sby = sg / g.nsegx, sgx = sg - sby * g.nsegx;
+    const int64_t b = a.b0 + bl;
+    const int j = sby * SBH + (lane / SBW);
+    int tx[SEGB], ty[SEGB];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int kk = wave * 4 + k;
-        const int64_t sbg = int64_t(wg) * kBinBlocks + kk;
+    for (int k = 0; k < SEGB; ++k) {
+        const int i = (sgx * SEGB + k) * SBW + (lane % SBW);
         tx[k] = ty[k] = -1;
-        if (sbg < nblk) {
-            const int bl = int(sbg / g.nsb);
-            const int sb = int(sbg - int64_t(bl) * g.nsb);
-            const int sby = sb / g.nsbx, sbx = sb - sby * g.nsbx;
-            const int i = sbx * SBW + (lane % SBW), j = sby * SBH + (lane / SBW);
-            if (lane == 0) { L.img[kk] = bl; L.sb[kk] = sb; }
-            if (i < W && j < H) {
-                typename Coords::V x, y;
-                co.load(a.b0 + bl, int64_t(j) * W + i, x, y);
-                co.target(i, j, x, y, H, W, tx[k], ty[k]);
-            }
-        } else if (lane == 0) {
-            L.img[kk] = -1;
+        if (i < W && j < H) {
+            typename Coords::V x, y;
+            co.load(b, int64_t(j) * W + i, x, y);
+            co.target(i, j, x, y, H, W, tx[k], ty[k]);
         }
     }
+    int s0x = 0x7FFFFFFF, s1x = -1, s0y = 0x7FFFFFFF, s1y = -1;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < SEGB; ++k) {
+        const int sbx = sgx * SEGB + k;
+        if (sbx >= g.nsbx) break;  // wave-uniform
         const bool ok = tx[k] >= 0;
-        const int mnx = wave_min(ok ? tx[k] : 0x7FFFFFFF), mxx = wave_max(ok ? tx[k] : -1);
-        const int mny = wave_min(ok ? ty[k] : 0x7FFFFFFF), mxy = wave_max(ok ? ty[k] : -1);
-        if (lane == 0) {
-            const int kk = wave * 4 + k;
-            if (mxx < 0) {
-                L.box[kk][0] = -1;
+        const int mxx = wave_max(ok ? tx[k] : -1);
+        ushort4 rec = empty_box();
+        if (mxx >= 0) {
+            const int t0x = wave_min(ok ? tx[k] : 0x7FFFFFFF) / TW, t1x = mxx / TW;
+            const int t0y = wave_min(ok ? ty[k] : 0x7FFFFFFF) / TH, t1y = wave_max(ok ? ty[k] : -1) / TH;
+            if ((t1x - t0x + 1) * (t1y - t0y + 1) > MAX_TILES_PER_BLOCK) {
+                // non-smooth flow: this block's sources go through the key slab
+                const int i = sbx * SBW + (lane % SBW);
+                const int64_t p = int64_t(j) * W + i;
+                const unsigned long long key = ok ? make_key(depth[b * HW + p], unsigned(p)) : 0ull;
+                wave_run_atomic_min(ws.keys + int64_t(bl) * HW, ok ? ty[k] * W + tx[k] : -1, key);
+                if (ok) ws.flag[int64_t(bl) * g.ntiles + (ty[k] / TH) * g.tilesX + tx[k] / TW] = 0u;
             } else {
-                const int t0x = mnx / TW, t1x = mxx / TW, t0y = mny / TH, t1y = mxy / TH;
-                const bool wide = (t1x - t0x + 1) * (t1y - t0y + 1) > MAX_TILES_PER_BLOCK;
-                L.box[kk][0] = wide ? -2 : t0x;
-                L.box[kk][1] = t1x;
-                L.box[kk][2] = t0y;
-                L.box[kk][3] = t1y;
+                rec = make_ushort4((unsigned short)t0x, (unsigned short)t1x, (unsigned short)t0y,
+                                   (unsigned short)t1y);
+                s0x = t0x < s0x ? t0x : s0x;
+                s1x = t1x > s1x ? t1x : s1x;
+                s0y = t0y < s0y ? t0y : s0y;
+                s1y = t1y > s1y ? t1y : s1y;
             }
         }
+        if (lane == 0) ws.blkrec[int64_t(bl) * g.nsb + int64_t(sby) * g.nsbx + sbx] = rec;
     }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int off = 0;
-        for (int k = 0; k < kBinBlocks; ++k) {
-            L.off[k] = off;
-            if (L.box[k][0] >= 0) off += (L.box[k][1] - L.box[k][0] + 1) * (L.box[k][3] - L.box[k][2] + 1);
-        }
-        L.off[kBinBlocks] = off;
-    }
-    __syncthreads();
-    if (threadIdx.x < kBinBlocks && L.box[threadIdx.x][0] >= 0) {
-        const int k = threadIdx.x;
-        int r = L.off[k];
-        for (int yt = L.box[k][2]; yt <= L.box[k][3]; ++yt)
-            for (int xt = L.box[k][0]; xt <= L.box[k][1]; ++xt, ++r) {
-                L.reg_tile[r] = L.img[k] * g.ntiles + yt * g.tilesX + xt;
-                L.reg_blk[r] = (unsigned char)k;
-            }
-    }
-    __syncthreads();
-    const int nreg = L.off[kBinBlocks];
-    int first = 0, rank = 0;
-    if (int(threadIdx.x) < nreg) {
-        const int r = threadIdx.x, T = L.reg_tile[r];
-        int tot = 0;
-        first = r;
-        for (int q = 0; q < nreg; ++q) {
-            if (L.reg_tile[q] == T) {
-                ++tot;
-                if (q < r) { ++rank; first = q < first ? q : first; }
-            }
-        }
-        if (rank == 0) L.base[r] = 0xFFFFFFFFu - atomicSub(ws.cnt + T, unsigned(tot));
-    }
-    __syncthreads();
-    if (int(threadIdx.x) < nreg) {
-        const int r = threadIdx.x, T = L.reg_tile[r];
-        const unsigned slot = L.base[first] + unsigned(rank);
-        L.slot[r] = slot;
-        if (slot < unsigned(CAP)) ws.list[int64_t(T) * CAP + slot] = unsigned(L.sb[L.reg_blk[r]]);
-    }
-    __syncthreads();
-    // ---- spills: wide boxes and list overflow go through the key slab
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int kk = wave * 4 + k;
-        if (L.img[kk] < 0 || L.box[kk][0] == -1) continue;  // wave-uniform
-        const int bl = L.img[kk];
-        const int sb = L.sb[kk];
-        const int sby = sb / g.nsbx, sbx = sb - sby * g.nsbx;
-        const int i = sbx * SBW + (lane % SBW), j = sby * SBH + (lane / SBW);
-        const int64_t b = a.b0 + bl, p = int64_t(j) * W + i;
-        const bool ok = tx[k] >= 0;
-        const int mytile = ok ? bl * g.ntiles + (ty[k] / TH) * g.tilesX + tx[k] / TW : -1;
-        unsigned long long *keys = ws.keys + int64_t(bl) * HW;
-        if (L.box[kk][0] == -2) {
-            const unsigned long long key = ok ? make_key(depth[b * HW + p], unsigned(p)) : 0ull;
-            wave_run_atomic_min(keys, ok ? ty[k] * W + tx[k] : -1, key);
-            if (ok) ws.flag[mytile] = 0u;
-            continue;
-        }
-        for (int r = L.off[kk]; r < L.off[kk + 1]; ++r) {
-            if (L.slot[r] < unsigned(CAP)) continue;
-            const int T = L.reg_tile[r];
-            const bool mine = mytile == T;
-            const unsigned long long key = mine ? make_key(depth[b * HW + p], unsigned(p)) : 0ull;
-            wave_run_atomic_min(keys, mine ? ty[k] * W + tx[k] : -1, key);
-            if (lane == 0) ws.flag[T] = 0u;
-        }
-    }
+    if (lane == 0)
+        ws.segrec[sgg] = s1x < 0 ? empty_box()
+                                 : make_ushort4((unsigned short)s0x, (unsigned short)s1x, (unsigned short)s0y,
+                                                (unsigned short)s1y);
 }
 
-// ---- TILE role: one workgroup per target tile.  Re-reads the listed source
-// blocks, folds their keys into the LDS z-buffer, merges the key slab if the
-// tile was flagged, then resolves the tile: gathers winners' channels and
-// writes output / valid / collision once with 16-byte stores.
-template <typename Coords>
+// ---- TILE role
+template <typename Coords, bool kStamp = false>
 __device__ __forceinline__ void tile_role(TileLds &L, int lin, const Coords &co, const float *__restrict__ obj,
                                           const float *__restrict__ depth, float *__restrict__ out,
                                           float *__restrict__ valid, float *__restrict__ coll,
                                           const ChunkArgs &a, int C, int H, int W, int64_t HW,
-                                          const TileGeom &g, int vec_ok) {
+                                          const TileGeom &g, unsigned long long *ph = nullptr) {
     const Ws &ws = a.ws;
     const int bl = lin / g.ntiles;
     const int tile = lin - bl * g.ntiles;
     const int tyi = tile / g.tilesX, txi = tile - tyi * g.tilesX;
     const int x0 = txi * TW, y0 = tyi * TH;
     const int64_t b = a.b0 + bl;
-    unsigned int *cnt = ws.cnt + lin;
-    unsigned int *flag = ws.flag + lin;
-    unsigned int *list = ws.list + int64_t(lin) * CAP;
     unsigned long long *keys = ws.keys + int64_t(bl) * HW;
+    const ushort4 *segrec = ws.segrec + int64_t(bl) * g.nseg;
+    const ushort4 *blkrec = ws.blkrec + int64_t(bl) * g.nsb;
 
     if (threadIdx.x == 0) {
-        const unsigned int c = 0xFFFFFFFFu - *cnt;
-        L.n = c < unsigned(CAP) ? c : unsigned(CAP);
-        L.flag = *flag;
-        *cnt = 0xFFFFFFFFu;  // restore the workspace invariant for the next call
-        *flag = 0xFFFFFFFFu;
+        L.flag = ws.flag[lin];
+        ws.flag[lin] = 0xFFFFFFFFu;  // restore the workspace invariant for the next call
+        L.nseg = 0;
+        L.nblk = 0;
     }
     for (int k = threadIdx.x; k < TW * TH; k += kWarpThreads) L.zk[k] = KEY_UNTOUCHED;
     __syncthreads();
-    const int n = int(L.n);
-    for (int k = threadIdx.x; k < n; k += kWarpThreads) {
-        L.list[k] = list[k];
-        list[k] = 0xFFFFFFFFu;
-    }
-    __syncthreads();
 
-    // ---- splat the listed source blocks into the LDS z-buffer
-    const int items = n * 64;
-    for (int w0 = threadIdx.x; w0 < items; w0 += kWarpThreads * kUnroll) {
-        typename Coords::V cx[kUnroll], cy[kUnroll];
-        float d[kUnroll];
-        int ii[kUnroll], jj[kUnroll];
-        bool live[kUnroll];
+    // ---- 1. segments whose box holds this tile (all loads of a thread in flight together)
+    for (int s0 = threadIdx.x; s0 < g.nseg; s0 += kWarpThreads * 4) {
+        ushort4 r[4];
 #pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
-            const int it = w0 + u * kWarpThreads;
-            live[u] = false;
-            if (it < items) {
-                const int sb = int(L.list[it >> 6]);
-                const int l = it & 63;
-                const int sby = sb / g.nsbx, sbx = sb - sby * g.nsbx;
-                ii[u] = sbx * SBW + (l % SBW);
-                jj[u] = sby * SBH + (l / SBW);
-                if (ii[u] < W && jj[u] < H) {
-                    live[u] = true;
-                    const int64_t p = int64_t(jj[u]) * W + ii[u];
-                    co.load(b, p, cx[u], cy[u]);
-                    d[u] = depth[b * HW + p];
-                }
+        for (int u = 0; u < 4; ++u) {
+            const int sidx = s0 + u * kWarpThreads;
+            r[u] = sidx < g.nseg ? segrec[sidx] : empty_box();
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (box_has(r[u], txi, tyi)) {
+                const unsigned idx = atomicAdd(&L.nseg, 1u);
+                if (idx < unsigned(kSegCap)) L.seg[idx] = unsigned(s0 + u * kWarpThreads);
             }
         }
-#pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
-            if (!live[u]) continue;
-            int tx, ty;
-            co.target(ii[u], jj[u], cx[u], cy[u], H, W, tx, ty);
-            const int lx = tx - x0, ly = ty - y0;
-            if (tx >= 0 && unsigned(lx) < unsigned(TW) && unsigned(ly) < unsigned(TH))
-                atomicMin(&L.zk[ly * TW + lx], make_key(d[u], unsigned(jj[u] * W + ii[u])));
-        }
     }
-    // ---- merge the global key slab where the bin pass spilled into it
+    __syncthreads();
+    if constexpr (kStamp) { if (threadIdx.x == 0) ph[4] = wall_clock64(); }
+    const int nsel = int(L.nseg);
+    // candidates: the blocks of the selected segments, or every block of the
+    // image if too many segments matched
+    const bool all_blocks = nsel > kSegCap;
+    const int ncand = all_blocks ? g.nsb : nsel * SEGB;
+
+    for (int c0 = 0; c0 < ncand; c0 += kListCap) {
+        // ---- 2. candidate blocks whose box holds this tile -> L.blk
+#pragma unroll
+        for (int u = 0; u < kListCap / kWarpThreads; ++u) {
+            const int c = c0 + int(threadIdx.x) + u * kWarpThreads;
+            int sb = -1;
+            if (c < ncand) {
+                if (all_blocks) {
+                    sb = c;
+                } else {
+                    const int sg = int(L.seg[c / SEGB]);
+                    const int sby = sg / g.nsegx, sbx = (sg - sby * g.nsegx) * SEGB + c % SEGB;
+                    sb = sbx < g.nsbx ? sby * g.nsbx + sbx : -1;
+                }
+            }
+            if (sb >= 0 && box_has(blkrec[sb], txi, tyi)) {
+                const unsigned idx = atomicAdd(&L.nblk, 1u);
+                L.blk[idx] = unsigned(sb);
+            }
+        }
+        __syncthreads();
+        // ---- 3. splat the selected blocks into the LDS z-buffer
+        const int items = int(L.nblk) * 64;
+        for (int w0 = threadIdx.x; w0 < items; w0 += kWarpThreads * kUnroll) {
+            typename Coords::V cx[kUnroll], cy[kUnroll];
+            float d[kUnroll];
+            int ii[kUnroll], jj[kUnroll];
+            bool live[kUnroll];
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                const int it = w0 + u * kWarpThreads;
+                live[u] = false;
+                if (it < items) {
+                    const int sb = int(L.blk[it >> 6]);
+                    const int l = it & 63;
+                    const int sby = sb / g.nsbx, sbx = sb - sby * g.nsbx;
+                    ii[u] = sbx * SBW + (l % SBW);
+                    jj[u] = sby * SBH + (l / SBW);
+                    if (ii[u] < W && jj[u] < H) {
+                        live[u] = true;
+                        const int64_t p = int64_t(jj[u]) * W + ii[u];
+                        co.load(b, p, cx[u], cy[u]);
+                        d[u] = depth[b * HW + p];
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                if (!live[u]) continue;
+                int tx, ty;
+                co.target(ii[u], jj[u], cx[u], cy[u], H, W, tx, ty);
+                const int lx = tx - x0, ly = ty - y0;
+                if (tx >= 0 && unsigned(lx) < unsigned(TW) && unsigned(ly) < unsigned(TH))
+                    atomicMin(&L.zk[ly * TW + lx], make_key(d[u], unsigned(jj[u] * W + ii[u])));
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) L.nblk = 0;
+        __syncthreads();
+    }
+    if constexpr (kStamp) { if (threadIdx.x == 0) ph[5] = wall_clock64(); }
+    // ---- 4. merge the key slab where the BIN role spilled into it
     if (L.flag == 0u) {
         for (int k = threadIdx.x; k < TW * TH; k += kWarpThreads) {
             const int ly = k / TW, lx = k - ly * TW;
@@ -475,66 +474,62 @@ __device__ __forceinline__ void tile_role(TileLds &L, int lin, const Coords &co,
                 }
             }
         }
+        __syncthreads();
     }
-    __syncthreads();
 
-    // ---- resolve: each thread owns kSteps groups of 4 consecutive targets;
-    // the gathers of up to kChan channels are all issued before any store, so
-    // one memory round trip covers 4 targets x kChan channels.  Offsets are
-    // 32-bit from the image base (C*H*W < 2^30 is checked on the host).
-    constexpr int kSteps = TW * TH / 4 / kWarpThreads;  // 2
-    constexpr int kChan = 8;
+    if constexpr (kStamp) { if (threadIdx.x == 0) { ph[6] = wall_clock64(); ph[7] = L.nseg; } }
+    // ---- 5. resolve.  Lane-strided: a wave covers 64 consecutive targets of
+    // one tile row, so every gather / store wave-instruction spans one
+    // contiguous row segment.  A thread owns kPer targets, handled kHalf at a
+    // time with all gathers of up to kChan channels in flight before any store.
+    // Offsets are 32-bit from the image base (C*H*W < 2^30 checked on the host).
+    constexpr int kPer = TW * TH / kWarpThreads;  // 8
+    constexpr int kHalf = 4;
+    constexpr int kChan = 4;
     const float *ob = obj + b * C * HW;
     float *oo = out + b * C * HW;
+    float *vb = valid + b * HW;
+    float *cb = coll + b * HW;
     const unsigned uHW = unsigned(HW);
 #pragma unroll
-    for (int s = 0; s < kSteps; ++s) {
-        const int q = threadIdx.x + s * kWarpThreads;
-        const int ly = (q * 4) / TW, lx = (q * 4) - ly * TW;
-        const int ty = y0 + ly, tx = x0 + lx;
-        if (ty >= H || tx >= W) continue;
-        const bool full = vec_ok && tx + 3 < W;
-        const unsigned t0 = unsigned(ty) * unsigned(W) + unsigned(tx);
-        const ulonglong2 k01 = *reinterpret_cast<const ulonglong2 *>(&L.zk[ly * TW + lx]);
-        const ulonglong2 k23 = *reinterpret_cast<const ulonglong2 *>(&L.zk[ly * TW + lx + 2]);
-        const unsigned long long key[4] = {k01.x, k01.y, k23.x, k23.y};
-        int src[4];
-        float vv[4], cc4[4];
+    for (int h = 0; h < kPer; h += kHalf) {
+        int src[kHalf];
+        unsigned t[kHalf];
+        bool live[kHalf];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const bool touched = key[k] != KEY_UNTOUCHED;
-            const bool nowin = key[k] == KEY_NOWIN;
-            vv[k] = touched ? 1.f : 0.f;
-            cc4[k] = nowin ? 1.f : 0.f;
-            src[k] = (touched && !nowin) ? int(key[k] & 0xFFFFFFFFull) : -1;
+        for (int k = 0; k < kHalf; ++k) {
+            const int q = int(threadIdx.x) + (h + k) * kWarpThreads;
+            const int ly = q / TW, lx = q - ly * TW;
+            const int ty = y0 + ly, tx = x0 + lx;
+            live[k] = ty < H && tx < W;
+            t[k] = unsigned(ty) * unsigned(W) + unsigned(tx);
+            const unsigned long long key = L.zk[q];
+            const bool touched = key != KEY_UNTOUCHED;
+            const bool nowin = key == KEY_NOWIN;
+            src[k] = (touched && !nowin) ? int(key & 0xFFFFFFFFull) : -1;
+            if (live[k]) {
+                vb[t[k]] = touched ? 1.f : 0.f;
+                cb[t[k]] = nowin ? 1.f : 0.f;
+            }
         }
         for (int c0 = 0; c0 < C; c0 += kChan) {
-            float o[kChan][4];
+            float o[kChan][kHalf];
 #pragma unroll
             for (int cc = 0; cc < kChan; ++cc) {
                 const bool chan = c0 + cc < C;
                 const unsigned pl = unsigned(c0 + cc) * uHW;
 #pragma unroll
-                for (int k = 0; k < 4; ++k) o[cc][k] = (chan && src[k] >= 0) ? ob[pl + unsigned(src[k])] : 0.f;
+                for (int k = 0; k < kHalf; ++k)
+                    o[cc][k] = (chan && src[k] >= 0) ? ob[pl + unsigned(src[k])] : 0.f;
             }
 #pragma unroll
             for (int cc = 0; cc < kChan; ++cc) {
                 if (c0 + cc >= C) break;
-                float *dst = oo + unsigned(c0 + cc) * uHW + t0;
-                if (full) {
-                    *reinterpret_cast<float4 *>(dst) = make_float4(o[cc][0], o[cc][1], o[cc][2], o[cc][3]);
-                } else {
-                    for (int k = 0; k < 4 && tx + k < W; ++k) dst[k] = o[cc][k];
-                }
+                float *dst = oo + unsigned(c0 + cc) * uHW;
+#pragma unroll
+                for (int k = 0; k < kHalf; ++k)
+                    if (live[k]) dst[t[k]] = o[cc][k];
             }
-        }
-        float *vd = valid + b * HW + t0;
-        float *cd = coll + b * HW + t0;
-        if (full) {
-            *reinterpret_cast<float4 *>(vd) = make_float4(vv[0], vv[1], vv[2], vv[3]);
-            *reinterpret_cast<float4 *>(cd) = make_float4(cc4[0], cc4[1], cc4[2], cc4[3]);
-        } else {
-            for (int k = 0; k < 4 && tx + k < W; ++k) { vd[k] = vv[k]; cd[k] = cc4[k]; }
         }
     }
 }
@@ -544,26 +539,38 @@ __device__ __forceinline__ void tile_role(TileLds &L, int lin, const Coords &co,
 // over the 8 XCDs (workgroups b and b+8 share one), so slot x = contiguous runs
 // per XCD keeps neighbouring tiles -- which share source blocks and gather
 // rows -- in one L2.  Placement only affects speed, never results.
-template <typename Coords>
-__global__ __launch_bounds__(kWarpThreads, 4) void warp_kernel(Coords co, const float *__restrict__ obj,
+template <typename Coords, bool kStamp = false>
+__global__ __launch_bounds__(kWarpThreads, 8) void warp_kernel(Coords co, const float *__restrict__ obj,
                                                                const float *__restrict__ depth,
                                                                float *__restrict__ out, float *__restrict__ valid,
                                                                float *__restrict__ coll, ChunkArgs tile_a,
                                                                ChunkArgs bin_a, int C, int H, int W, int64_t HW,
-                                                               TileGeom g, int vec_ok) {
+                                                               TileGeom g, unsigned long long *stamps = nullptr) {
     __shared__ WarpLds lds;
     const unsigned N = unsigned(tile_a.nwg + bin_a.nwg);
     const unsigned per = (N + 7u) / 8u;
     const unsigned x = (blockIdx.x % 8u) * per + blockIdx.x / 8u;
     if (x >= N) return;
+    unsigned long long t_start = 0;
+    if constexpr (kStamp) t_start = wall_clock64();  // diagnostic build only (tools/probe_tile)
     // number of BIN slots among [0, x) at an even stride
     const unsigned nb0 = unsigned((uint64_t(x) * unsigned(bin_a.nwg)) / N);
     const unsigned nb1 = unsigned((uint64_t(x + 1) * unsigned(bin_a.nwg)) / N);
-    if (nb1 > nb0) {
-        bin_role<Coords>(lds.bin, int(nb0), co, depth, bin_a, H, W, HW, g);
+    const bool is_bin = nb1 > nb0;
+    if (is_bin) {
+        bin_role<Coords>(int(nb0), co, depth, bin_a, H, W, HW, g);
     } else {
-        tile_role<Coords>(lds.tile, int(x - nb0), co, obj, depth, out, valid, coll, tile_a, C, H, W, HW, g,
-                          vec_ok);
+        tile_role<Coords, kStamp>(lds.tile, int(x - nb0), co, obj, depth, out, valid, coll, tile_a, C, H, W, HW, g,
+                                  kStamp ? stamps + 8 * x : nullptr);
+    }
+    if constexpr (kStamp) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            stamps[8 * x + 0] = t_start;
+            stamps[8 * x + 1] = wall_clock64();
+            stamps[8 * x + 2] = is_bin ? 1 : 0;
+            stamps[8 * x + 3] = is_bin ? nb0 : x - nb0;
+        }
     }
 }
 
@@ -719,6 +726,34 @@ int zero_masks(void *valid, void *coll, size_t bytes, hipStream_t st) {
     return e == hipSuccess ? OFD_FW_OK : int(e);
 }
 
+// Which slab layout last left each workspace's key slabs and flags
+// all-ones.  A workspace initialised by ofd_fw_workspace_init is clean for
+// every layout; a call with a different layout (other H, W or chunking) than
+// the last one re-initialises the slabs it uses before launching, because the
+// previous layout's scratch boxes may sit where this layout keeps keys/flags.
+struct LayoutSig {
+    int64_t H, W, G;
+    int nslab;
+    bool operator==(const LayoutSig &o) const { return H == o.H && W == o.W && G == o.G && nslab == o.nslab; }
+};
+constexpr LayoutSig kCleanSig{-1, -1, -1, -1};
+std::mutex g_layout_mu;
+std::unordered_map<const void *, LayoutSig> g_layout;
+
+void mark_clean(const void *ws) {
+    std::lock_guard<std::mutex> lk(g_layout_mu);
+    g_layout[ws] = kCleanSig;
+}
+
+// true if the caller must re-initialise the slabs before using layout `sig`
+bool claim_layout(const void *ws, const LayoutSig &sig) {
+    std::lock_guard<std::mutex> lk(g_layout_mu);
+    auto it = g_layout.find(ws);
+    const bool ok = it != g_layout.end() && (it->second == sig || it->second == kCleanSig);
+    g_layout[ws] = sig;
+    return !ok;
+}
+
 template <typename Coords>
 int run_f32(Coords co, const float *obj, const float *depth, float *out, float *valid, float *coll,
             int64_t B, int64_t C, int64_t H, int64_t W, void *ws, size_t ws_bytes, hipStream_t st) {
@@ -728,50 +763,55 @@ int run_f32(Coords co, const float *obj, const float *depth, float *out, float *
     if (!ws || !aligned(ws, 16)) return OFD_FW_EWORKSPACE;
     const size_t per_image = per_image_bytes(H, W);
     const TileGeom g = make_geom(H, W);
-    const int vec_ok = (W % 4 == 0) && aligned(out, 16) && aligned(valid, 16) && aligned(coll, 16);
     // the tile engine's gathers use 32-bit offsets inside one image
     const Mode mode = (C * HW < (int64_t(1) << 30)) ? engine_mode() : Mode::Atomic;
 
+    // Slab layout (shared by both engines so the all-ones key / flag regions
+    // are the same bytes whichever engine ran last): two slabs when they fit,
+    // chunk c in slab c % 2; otherwise one slab.
+    int64_t G = chunk_images(B, HW, per_image, ws_bytes / 2);
+    int nslab = 2;
+    if (G < 1 || G >= B) {
+        G = chunk_images(B, HW, per_image, ws_bytes);
+        nslab = 1;
+    }
+    if (G < 1) return OFD_FW_EWORKSPACE;
+    const int64_t nch = (B + G - 1) / G;
+    if (claim_layout(ws, LayoutSig{H, W, G, nslab})) {
+        const hipError_t e = hipMemsetAsync(ws, 0xFF, size_t(nslab) * size_t(G) * per_image, st);
+        if (e != hipSuccess) return int(e);
+    }
+    Ws slab[2];
+    slab[0] = carve(ws, G, HW, g);
+    slab[1] = carve(static_cast<char *>(ws) + size_t(G) * per_image, G, HW, g);
+
     if (mode == Mode::Atomic) {
-        const int64_t G = chunk_images(B, HW, per_image, ws_bytes);
-        if (G < 1) return OFD_FW_EWORKSPACE;
-        auto *keys = static_cast<unsigned long long *>(ws);
-        for (int64_t b0 = 0; b0 < B; b0 += G) {
+        for (int64_t c = 0; c < nch; ++c) {
+            const int64_t b0 = c * G;
             const int64_t nb = (B - b0) < G ? (B - b0) : G;
             const int64_t px = nb * HW;
+            unsigned long long *keys = slab[nslab == 2 ? c % 2 : 0].keys;
             hipLaunchKernelGGL((splat_atomic_kernel<Coords>), dim3(grid_for(px, kBlock * 4)), dim3(kBlock), 0, st,
                                co, depth, keys, int(H), int(W), HW, b0, px);
             hipLaunchKernelGGL(resolve_atomic_kernel, dim3(grid_for(px, kBlock * 4)), dim3(kBlock), 0, st,
                                obj, keys, out, valid, coll, int(C), HW, b0, px);
         }
     } else {
-        // Two slabs when they fit: chunk c uses slab c % 2, and launch L runs
-        // TILE(chunk L-1) beside BIN(chunk L).  One slab: BIN and TILE launches
-        // alternate.
-        int64_t G = chunk_images(B, HW, per_image, ws_bytes / 2);
-        int nslab = 2;
-        if (G < 1 || G >= B) {
-            G = chunk_images(B, HW, per_image, ws_bytes);
-            nslab = 1;
-        }
-        if (G < 1) return OFD_FW_EWORKSPACE;
-        const int64_t nch = (B + G - 1) / G;
-        Ws slab[2];
-        slab[0] = carve(ws, G, HW, g);
-        slab[1] = carve(static_cast<char *>(ws) + size_t(G) * per_image, G, HW, g);
+        // launch L runs TILE(chunk L-1) beside BIN(chunk L); with one slab the
+        // BIN and TILE launches alternate.
         auto chunk = [&](int64_t c, int role_bin) {
             ChunkArgs a;
             a.ws = slab[nslab == 2 ? c % 2 : 0];
             a.b0 = c * G;
             a.nimg = int((B - a.b0) < G ? (B - a.b0) : G);
-            a.nwg = role_bin ? int((int64_t(a.nimg) * g.nsb + kBinBlocks - 1) / kBinBlocks) : a.nimg * g.ntiles;
+            a.nwg = role_bin ? int((int64_t(a.nimg) * g.nseg + kWaves - 1) / kWaves) : a.nimg * g.ntiles;
             return a;
         };
         ChunkArgs none{};
         auto launch = [&](const ChunkArgs &t, const ChunkArgs &b) {
             const unsigned N = unsigned(t.nwg + b.nwg);
             hipLaunchKernelGGL((warp_kernel<Coords>), dim3((N + 7u) / 8u * 8u), dim3(kWarpThreads), 0, st,
-                               co, obj, depth, out, valid, coll, t, b, int(C), int(H), int(W), HW, g, vec_ok);
+                               co, obj, depth, out, valid, coll, t, b, int(C), int(H), int(W), HW, g);
         };
         if (nslab == 2) {
             for (int64_t L = 0; L <= nch; ++L)
@@ -827,6 +867,7 @@ int ofd_fw_workspace_init(void *workspace, size_t bytes, void *stream) {
     if (!workspace && bytes) return OFD_FW_EINVAL;
     if (!bytes) return OFD_FW_OK;
     const hipError_t e = hipMemsetAsync(workspace, 0xFF, bytes, static_cast<hipStream_t>(stream));
+    if (e == hipSuccess) mark_clean(workspace);
     return e == hipSuccess ? OFD_FW_OK : int(e);
 }
 
@@ -882,6 +923,12 @@ int ofd_fw_forward_warping_f64(const double *obj, const double *safe_y, const do
     if (G < 1) return OFD_FW_EWORKSPACE;
     auto *zkeys = static_cast<unsigned long long *>(workspace);
     auto *idx = reinterpret_cast<unsigned int *>(zkeys + G * HW);
+    // The f32 engines keep scratch records in parts of the shared workspace,
+    // so the float64 op (a rare path) initialises the region it uses.
+    {
+        const hipError_t e = hipMemsetAsync(workspace, 0xFF, size_t(G) * per_image, st);
+        if (e != hipSuccess) return int(e);
+    }
     for (int64_t b0 = 0; b0 < B; b0 += G) {
         const int64_t nb = (B - b0) < G ? (B - b0) : G;
         const int64_t px = nb * HW;

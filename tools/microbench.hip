@@ -9,6 +9,24 @@
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
 
+template <int U>
+__global__ __launch_bounds__(256) void copyU(const float4* __restrict__ a, float4* __restrict__ b, size_t n) {
+    size_t base = (blockIdx.x * (size_t)256 * U) + threadIdx.x;
+    float4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) if (base + u * 256 < n) v[u] = a[base + u * 256];
+#pragma unroll
+    for (int u = 0; u < U; ++u) if (base + u * 256 < n) b[base + u * 256] = v[u];
+}
+
+__global__ __launch_bounds__(256) void read4(const float4* __restrict__ a, float* out, size_t n) {
+    size_t base = (blockIdx.x * (size_t)256 * 4) + threadIdx.x;
+    float acc = 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) { float4 v = a[base + u * 256]; acc += v.x + v.y + v.z + v.w; }
+    if (acc == 12345.f) out[0] = acc;
+}
+
 __global__ void copy4(const float4* __restrict__ a, float4* __restrict__ b, size_t n) {
     size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     size_t st = (size_t)gridDim.x * blockDim.x;
@@ -62,6 +80,15 @@ int main() {
     CK(hipMemset(a, 0, n * 16));
     float ms = timeit([&] { copy4<<<2048 * 4, 256>>>(a, b, n); });
     printf("copy float4 1GiB->1GiB: %.3f ms  %.1f GB/s (read+write)\n", ms, 2.0 * n * 16 / ms / 1e6);
+    ms = timeit([&] { copyU<1><<<n / 256, 256>>>(a, b, n); });
+    printf("copyU<1> : %.3f ms  %.1f GB/s\n", ms, 2.0 * n * 16 / ms / 1e6);
+    ms = timeit([&] { copyU<4><<<n / 1024, 256>>>(a, b, n); });
+    printf("copyU<4> : %.3f ms  %.1f GB/s\n", ms, 2.0 * n * 16 / ms / 1e6);
+    ms = timeit([&] { copyU<8><<<n / 2048, 256>>>(a, b, n); });
+    printf("copyU<8> : %.3f ms  %.1f GB/s\n", ms, 2.0 * n * 16 / ms / 1e6);
+    float* o1; CK(hipMalloc(&o1, 64));
+    ms = timeit([&] { read4<<<n / 1024, 256>>>(a, o1, n); });
+    printf("read-only: %.3f ms  %.1f GB/s\n", ms, 1.0 * n * 16 / ms / 1e6);
     (void)n4;
 
     const size_t NA = 50331648;  // one headline step of sources
