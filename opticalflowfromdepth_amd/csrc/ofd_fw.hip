@@ -66,12 +66,14 @@ constexpr int TW = 128, TH = 32;          // target tile (LDS z-buffer 32 KiB)
 constexpr int SBW = 16, SBH = 4;          // source block = one wave (64 px)
 constexpr int SEGB = 8;                   // source blocks per segment (128 x 4 px)
 constexpr int MAX_TILES_PER_BLOCK = 12;   // wider boxes go through the global path
-constexpr int kUnroll = 4;                // source pixels in flight per thread
+constexpr int kSplatU = 8;                // source blocks in flight per wave (tile role)
 
-// Default chunk: 4 images of 768x1024 (26 MB of slab); a chunk's re-read
-// flow/depth planes (12 B/px) stay resident in the 256 MiB Infinity Cache
-// between its BIN and TILE roles.
-constexpr size_t kDefaultChunkBytes = size_t(26) << 20;
+// Default chunk: 24M source pixels (32 images of 768x1024).  Big chunks give
+// each launch many more workgroups than resident slots, so the workgroups'
+// latency-bound scan/splat phases interleave with other workgroups'
+// bandwidth-bound resolve phases (measured: 4 / 8 / 16 / 32 images per chunk
+// = 1.44 / 1.27 / 1.14 / 0.99 ms per 64-image step).
+constexpr size_t kDefaultChunkPixels = size_t(24) << 20;
 
 // ---------------------------------------------------------------- key helpers
 // Monotone map float -> uint32 (total order of non-NaN floats), -0 == +0.
@@ -420,39 +422,43 @@ __device__ __forceinline__ void tile_role(TileLds &L, int lin, const Coords &co,
             }
         }
         __syncthreads();
-        // ---- 3. splat the selected blocks into the LDS z-buffer
-        const int items = int(L.nblk) * 64;
-        for (int w0 = threadIdx.x; w0 < items; w0 += kWarpThreads * kUnroll) {
-            typename Coords::V cx[kUnroll], cy[kUnroll];
-            float d[kUnroll];
-            int ii[kUnroll], jj[kUnroll];
-            bool live[kUnroll];
+        // ---- 3. splat the selected blocks into the LDS z-buffer.  One wave per
+        // source block (block id wave-uniform, pixel = lane), kSplatU blocks in
+        // flight per wave: every lane holds 3*kSplatU loads at once.
+        const int nb = int(L.nblk);
+        const int lane = lane_id(), wave = threadIdx.x >> 6;
+        for (int e0 = wave; e0 < nb; e0 += kWaves * kSplatU) {
+            typename Coords::V cx[kSplatU], cy[kSplatU];
+            float d[kSplatU];
 #pragma unroll
-            for (int u = 0; u < kUnroll; ++u) {
-                const int it = w0 + u * kWarpThreads;
-                live[u] = false;
-                if (it < items) {
-                    const int sb = int(L.blk[it >> 6]);
-                    const int l = it & 63;
+            for (int u = 0; u < kSplatU; ++u) {
+                const int e = e0 + u * kWaves;
+                cx[u] = cy[u] = typename Coords::V(0);
+                d[u] = 0.f;
+                if (e < nb) {
+                    const int sb = __builtin_amdgcn_readfirstlane(int(L.blk[e]));
                     const int sby = sb / g.nsbx, sbx = sb - sby * g.nsbx;
-                    ii[u] = sbx * SBW + (l % SBW);
-                    jj[u] = sby * SBH + (l / SBW);
-                    if (ii[u] < W && jj[u] < H) {
-                        live[u] = true;
-                        const int64_t p = int64_t(jj[u]) * W + ii[u];
+                    const int i = sbx * SBW + (lane % SBW), j = sby * SBH + (lane / SBW);
+                    if (i < W && j < H) {
+                        const int64_t p = int64_t(j) * W + i;
                         co.load(b, p, cx[u], cy[u]);
                         d[u] = depth[b * HW + p];
                     }
                 }
             }
 #pragma unroll
-            for (int u = 0; u < kUnroll; ++u) {
-                if (!live[u]) continue;
+            for (int u = 0; u < kSplatU; ++u) {
+                const int e = e0 + u * kWaves;
+                if (e >= nb) break;  // wave-uniform
+                const int sb = __builtin_amdgcn_readfirstlane(int(L.blk[e]));
+                const int sby = sb / g.nsbx, sbx = sb - sby * g.nsbx;
+                const int i = sbx * SBW + (lane % SBW), j = sby * SBH + (lane / SBW);
+                if (i >= W || j >= H) continue;
                 int tx, ty;
-                co.target(ii[u], jj[u], cx[u], cy[u], H, W, tx, ty);
+                co.target(i, j, cx[u], cy[u], H, W, tx, ty);
                 const int lx = tx - x0, ly = ty - y0;
                 if (tx >= 0 && unsigned(lx) < unsigned(TW) && unsigned(ly) < unsigned(TH))
-                    atomicMin(&L.zk[ly * TW + lx], make_key(d[u], unsigned(jj[u] * W + ii[u])));
+                    atomicMin(&L.zk[ly * TW + lx], make_key(d[u], unsigned(j * W + i)));
             }
         }
         __syncthreads();
@@ -856,7 +862,7 @@ size_t ofd_fw_workspace_bytes(int64_t B, int64_t H, int64_t W, int f64) {
     const size_t per_image = per_image_bytes(H, W);
     // chunk = the images whose slabs and re-read planes stay cache-resident
     // between a chunk's BIN and TILE roles; OFD_FW_CHUNK_IMAGES overrides.
-    size_t g = kDefaultChunkBytes / per_image;
+    size_t g = kDefaultChunkPixels / (size_t(H) * size_t(W));
     if (const char *e = getenv("OFD_FW_CHUNK_IMAGES")) g = size_t(atoi(e));
     if (g < 1) g = 1;
     if (g >= size_t(B)) return size_t(B) * per_image;  // one chunk, one slab

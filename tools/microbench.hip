@@ -27,6 +27,44 @@ __global__ __launch_bounds__(256) void read4(const float4* __restrict__ a, float
     if (acc == 12345.f) out[0] = acc;
 }
 
+__global__ __launch_bounds__(256) void copy1(const float* __restrict__ a, float* __restrict__ b, size_t n) {
+    size_t i = blockIdx.x * (size_t)256 + threadIdx.x;
+    if (i < n) b[i] = a[i];
+}
+
+// resolve-like: per target read a u32 source index, gather C planes, write C + 2 planes
+template <int C, int PER>
+__global__ __launch_bounds__(256) void resolve_sim(const unsigned* __restrict__ idx, const float* __restrict__ obj,
+                                                    float* __restrict__ out, size_t hw, size_t n) {
+    size_t t0 = blockIdx.x * (size_t)256 * PER + threadIdx.x;
+#pragma unroll
+    for (int p = 0; p < PER; ++p) {
+        size_t t = t0 + p * 256;
+        if (t >= n) return;
+        size_t img = t / hw, pix = t - img * hw;
+        unsigned s = idx[t];
+        const float* ob = obj + img * C * hw;
+        float* oo = out + img * (C + 2) * hw + pix;
+        float v[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) v[c] = ob[c * hw + s];
+#pragma unroll
+        for (int c = 0; c < C; ++c) oo[c * hw] = v[c];
+        oo[C * hw] = 1.f;
+        oo[(C + 1) * hw] = 0.f;
+    }
+}
+
+__global__ void init_idx(unsigned* idx, size_t hw, size_t n) {
+    size_t t = blockIdx.x * (size_t)256 + threadIdx.x;
+    if (t >= n) return;
+    size_t pix = t % hw;
+    long s = (long)pix + 17 - (long)((pix / 1024) % 7);   // coherent, shifted sources
+    if (s < 0) s = 0;
+    if (s >= (long)hw) s = hw - 1;
+    idx[t] = (unsigned)s;
+}
+
 __global__ void copy4(const float4* __restrict__ a, float4* __restrict__ b, size_t n) {
     size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     size_t st = (size_t)gridDim.x * blockDim.x;
@@ -86,6 +124,18 @@ int main() {
     printf("copyU<4> : %.3f ms  %.1f GB/s\n", ms, 2.0 * n * 16 / ms / 1e6);
     ms = timeit([&] { copyU<8><<<n / 2048, 256>>>(a, b, n); });
     printf("copyU<8> : %.3f ms  %.1f GB/s\n", ms, 2.0 * n * 16 / ms / 1e6);
+    ms = timeit([&] { copy1<<<n * 4 / 256, 256>>>((const float*)a, (float*)b, n * 4); });
+    printf("copy1 (dword/lane): %.3f ms  %.1f GB/s\n", ms, 2.0 * n * 16 / ms / 1e6);
+    {
+        const size_t hw = 768 * 1024, nimg = 32, npx = hw * nimg;
+        unsigned* idx; float* obj; float* out;
+        CK(hipMalloc(&idx, npx * 4)); CK(hipMalloc(&obj, npx * 6 * 4)); CK(hipMalloc(&out, npx * 8 * 4));
+        init_idx<<<npx / 256, 256>>>(idx, hw, npx);
+        float m1 = timeit([&] { resolve_sim<6, 1><<<npx / 256, 256>>>(idx, obj, out, hw, npx); });
+        float m4 = timeit([&] { resolve_sim<6, 4><<<npx / 1024, 256>>>(idx, obj, out, hw, npx); });
+        const double bytes = npx * (4.0 + 24 + 32);
+        printf("resolve_sim C=6 (60 B/px): PER=1 %.3f ms %.1f GB/s | PER=4 %.3f ms %.1f GB/s\n", m1, bytes / m1 / 1e6, m4, bytes / m4 / 1e6);
+    }
     float* o1; CK(hipMalloc(&o1, 64));
     ms = timeit([&] { read4<<<n / 1024, 256>>>(a, o1, n); });
     printf("read-only: %.3f ms  %.1f GB/s\n", ms, 1.0 * n * 16 / ms / 1e6);
