@@ -68,12 +68,11 @@ constexpr int SEGB = 8;                   // source blocks per segment (128 x 4 
 constexpr int MAX_TILES_PER_BLOCK = 12;   // wider boxes go through the global path
 constexpr int kSplatU = 8;                // source blocks in flight per wave (tile role)
 
-// Default chunk: 24M source pixels (32 images of 768x1024).  Big chunks give
-// each launch many more workgroups than resident slots, so the workgroups'
-// latency-bound scan/splat phases interleave with other workgroups'
-// bandwidth-bound resolve phases (measured: 4 / 8 / 16 / 32 images per chunk
-// = 1.44 / 1.27 / 1.14 / 0.99 ms per 64-image step).
-constexpr size_t kDefaultChunkPixels = size_t(24) << 20;
+// Default chunk: 64M source pixels (85 images of 768x1024, a ~830 MB slab).
+// Every kernel of a chunk then has a grid many times the resident slots
+// (measured per 64-image step: 16 / 32 / 64-image chunks = 1.15 / 1.05 / 1.02
+// ms of summed launches).
+constexpr size_t kDefaultChunkPixels = size_t(64) << 20;
 
 // ---------------------------------------------------------------- key helpers
 // Monotone map float -> uint32 (total order of non-NaN floats), -0 == +0.
@@ -153,23 +152,25 @@ struct FlowCoords {  // FW.forward input: flow [B,2,H,W], ch0 = x, ch1 = y
 // ---------------------------------------------------------------- wave helpers
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
-// Wave-wide min / max with DPP row operations (no LDS round trip): quad
-// swaps, row mirrors, then the row_bcast:15 / row_bcast:31 steps fold the four
-// 16-lane rows into lane 63, which readlane broadcasts.
-template <bool kMin>
-__device__ __forceinline__ int wave_reduce(int v) {
-    constexpr int ident = kMin ? 0x7FFFFFFF : int(0x80000000);
-    auto op = [](int a, int b) { return kMin ? (a < b ? a : b) : (a > b ? a : b); };
-    v = op(v, __builtin_amdgcn_update_dpp(ident, v, 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
-    v = op(v, __builtin_amdgcn_update_dpp(ident, v, 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
-    v = op(v, __builtin_amdgcn_update_dpp(ident, v, 0x141, 0xF, 0xF, false));  // row_half_mirror
-    v = op(v, __builtin_amdgcn_update_dpp(ident, v, 0x140, 0xF, 0xF, false));  // row_mirror
-    v = op(v, __builtin_amdgcn_update_dpp(ident, v, 0x142, 0xA, 0xF, false));  // row_bcast:15
-    v = op(v, __builtin_amdgcn_update_dpp(ident, v, 0x143, 0xC, 0xF, false));  // row_bcast:31
-    return __builtin_amdgcn_readlane(v, 63);
+// Wave-wide min of two packed unsigned 16-bit values (v_pk_min_u16) with DPP
+// row operations (no LDS round trip): quad swaps and row mirrors reduce each
+// 16-lane row, then row_bcast:15 / row_bcast:31 fold the four rows into lane
+// 63, which readlane broadcasts.  One reduction yields (min lo, min hi).
+__device__ __forceinline__ unsigned pk_min_u16(unsigned a, unsigned b) {
+    unsigned r;
+    asm volatile("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
 }
-__device__ __forceinline__ int wave_min(int v) { return wave_reduce<true>(v); }
-__device__ __forceinline__ int wave_max(int v) { return wave_reduce<false>(v); }
+__device__ __forceinline__ unsigned wave_min_pk16(unsigned v) {
+    constexpr int ident = -1;  // 0xFFFF in both halves
+    v = pk_min_u16(v, unsigned(__builtin_amdgcn_update_dpp(ident, int(v), 0xB1, 0xF, 0xF, false)));
+    v = pk_min_u16(v, unsigned(__builtin_amdgcn_update_dpp(ident, int(v), 0x4E, 0xF, 0xF, false)));
+    v = pk_min_u16(v, unsigned(__builtin_amdgcn_update_dpp(ident, int(v), 0x141, 0xF, 0xF, false)));
+    v = pk_min_u16(v, unsigned(__builtin_amdgcn_update_dpp(ident, int(v), 0x140, 0xF, 0xF, false)));
+    v = pk_min_u16(v, unsigned(__builtin_amdgcn_update_dpp(ident, int(v), 0x142, 0xA, 0xF, false)));
+    v = pk_min_u16(v, unsigned(__builtin_amdgcn_update_dpp(ident, int(v), 0x143, 0xC, 0xF, false)));
+    return unsigned(__builtin_amdgcn_readlane(int(v), 63));
+}
 
 // Global atomic min of `key` into base[t] for every lane with t >= 0, issuing
 // one atomic per run of consecutive lanes with the same t (border clamping
@@ -219,18 +220,20 @@ inline TileGeom make_geom(int64_t H, int64_t W) {
 
 inline size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
-// Per-image workspace: key slab (HW u64, only touched by spills), per-tile
-// spill flags, and the target-tile boxes of every source segment and block.
+// Per-image workspace: key slab (HW u64, only touched by spills), winner map
+// (HW u32), per-tile spill flags, and the target-tile boxes of every source
+// segment and block.
 inline size_t per_image_bytes(int64_t H, int64_t W) {
     const TileGeom g = make_geom(H, W);
-    return size_t(H) * size_t(W) * 8 + size_t(g.ntiles) * 4 + size_t(g.nseg) * 8 + size_t(g.nsb) * 8 + 48;
+    return size_t(H) * size_t(W) * 12 + size_t(g.ntiles) * 4 + size_t(g.nseg) * 8 + size_t(g.nsb) * 8 + 64;
 }
 
 struct Ws {  // views of one chunk's workspace (G images)
     unsigned long long *keys;  // [G][HW]      KEY_UNTOUCHED between calls
+    unsigned int *winner;      // [G][HW]      scratch: winning source index, ~0 = none
     unsigned int *flag;        // [G][ntiles]  0 = merge key slab, ~0 = clean
-    ushort4 *segrec;           // [G][nseg]    target tile box (t0x,t1x,t0y,t1y) of a segment
-    ushort4 *blkrec;           // [G][nsb]     same per source block
+    ushort4 *segrec;           // [G][nseg]    scratch: target tile box (t0x,t1x,t0y,t1y) of a segment
+    ushort4 *blkrec;           // [G][nsb]     scratch: same per source block
 };
 
 inline Ws carve(void *ws, int64_t G, int64_t HW, const TileGeom &g) {
@@ -238,6 +241,8 @@ inline Ws carve(void *ws, int64_t G, int64_t HW, const TileGeom &g) {
     char *p = static_cast<char *>(ws);
     w.keys = reinterpret_cast<unsigned long long *>(p);
     p += align16(size_t(G) * size_t(HW) * 8);
+    w.winner = reinterpret_cast<unsigned int *>(p);
+    p += align16(size_t(G) * size_t(HW) * 4);
     w.flag = reinterpret_cast<unsigned int *>(p);
     p += align16(size_t(G) * g.ntiles * 4);
     w.segrec = reinterpret_cast<ushort4 *>(p);
@@ -253,26 +258,32 @@ __device__ __forceinline__ bool box_has(const ushort4 &r, int tx, int ty) {
 }
 
 // ---------------------------------------------------------------- TILE engine
-// One fused, pipelined kernel per chunk boundary: launch L runs the TILE role
-// for chunk L-1 and the BIN role for chunk L side by side (their workspace
-// slabs alternate), roles interleaved evenly over the grid.
+// Three kernels per chunk of images, each with a grid far larger than the
+// resident slots:
 //
-// BIN  : one wave per source segment (SEGB blocks of 16x4 px).  Streams the
-//        flow, writes each block's target-tile box and the segment's union box.
-//        No atomics, no lists: a pure streaming pass.  A block whose box spans
-//        more than MAX_TILES_PER_BLOCK tiles (non-smooth flow) is not boxed: its
-//        sources go to the key slab by global atomic min (pre-reduced over runs
-//        of equal targets) and flag their target tiles.
-// TILE : one workgroup per target tile.  Finds its source blocks by scanning
-//        the segment boxes of the image, then the block boxes of the selected
-//        segments (both L2-resident), folds the selected blocks' keys into an
-//        LDS z-buffer (ds_min_u64), merges the key slab if flagged, and
-//        resolves: gathers the winners' channels, writes output / valid /
-//        collision exactly once.
+// BIN     : one wave per source segment (SEGB blocks of 16x4 px).  Streams the
+//           flow, writes each block's target-tile box and the segment's union
+//           box.  No atomics, no lists.  A block whose box spans more than
+//           MAX_TILES_PER_BLOCK tiles (non-smooth flow) is not boxed: its
+//           sources go to the key slab by global atomic min (pre-reduced over
+//           runs of equal targets) and flag their target tiles.
+// SPLAT   : one workgroup per 128x32 target tile.  Finds its source blocks by
+//           scanning the segment boxes of the image, then the block boxes of
+//           the selected segments (both L2-resident), folds the selected
+//           blocks' keys into an LDS z-buffer (ds_min_u64), merges the key
+//           slab if flagged, and publishes the tile: winner index (u32),
+//           valid, collision.
+// RESOLVE : one target per thread, lane-consecutive: reads the winner index
+//           and gathers / writes the C channels.  A pure streaming kernel
+//           (tools/microbench.hip resolve_sim: 5.9 TB/s on this access shape,
+//           against ~4.4 TB/s when the resolve ran inside the tile workgroup
+//           behind its latency-bound scan / splat phases).
 constexpr int kWarpThreads = 512;
 constexpr int kWaves = kWarpThreads / 64;
 constexpr int kSegCap = 768;    // selected segments held in LDS (else: scan all blocks)
 constexpr int kListCap = 1024;  // candidate blocks examined per batch
+constexpr int kResolveThreads = 256;
+constexpr unsigned int WIN_NONE = 0xFFFFFFFFu;
 
 struct TileLds {
     unsigned long long zk[TW * TH];
@@ -281,24 +292,19 @@ struct TileLds {
     unsigned int nseg, nblk, flag;
 };
 
-union __align__(16) WarpLds {
-    TileLds tile;
-};
-
-struct ChunkArgs {  // one chunk's share of a launch
+struct ChunkArgs {  // one chunk of images
     Ws ws;
     int64_t b0;     // first image of the chunk
     int nimg;       // images in the chunk
-    int nwg;        // workgroups of this role in the launch
 };
 
-// ---- BIN role: wave w of workgroup wg boxes segment wg * kWaves + w.
+// ---- BIN: wave w of workgroup blockIdx.x boxes segment blockIdx.x * kWaves + w.
 template <typename Coords>
-__device__ __forceinline__ void bin_role(int wg, const Coords &co, const float *__restrict__ depth,
-                                         const ChunkArgs &a, int H, int W, int64_t HW, const TileGeom &g) {
+__global__ __launch_bounds__(kWarpThreads) void bin_kernel(Coords co, const float *__restrict__ depth, ChunkArgs a,
+                                                           int H, int W, int64_t HW, TileGeom g) {
     const Ws &ws = a.ws;
     const int lane = lane_id();
-    const int64_t sgg = int64_t(wg) * kWaves + (threadIdx.x >> 6);
+    const int64_t sgg = int64_t(blockIdx.x) * kWaves + (threadIdx.x >> 6);
     if (sgg >= int64_t(a.nimg) * g.nseg) return;  // wave-uniform
     const int bl = int(sgg / g.nseg);
     const int sg = int(sgg - int64_t(bl) * g.nseg);
@@ -322,18 +328,22 @@ __device__ __forceinline__ void bin_role(int wg, const Coords &co, const float *
         const int sbx = sgx * SEGB + k;
         if (sbx >= g.nsbx) break;  // wave-uniform
         const bool ok = tx[k] >= 0;
-        const int mxx = wave_max(ok ? tx[k] : -1);
+        // tile-unit box: min over (tile x, tile y) and over (0xFFFF - tile x,
+        // 0xFFFF - tile y), two packed 16-bit reductions
+        const unsigned ttx = ok ? unsigned(tx[k] / TW) : 0xFFFFu, tty = ok ? unsigned(ty[k] / TH) : 0xFFFFu;
+        const unsigned mn = wave_min_pk16(ttx | (tty << 16));
+        const unsigned mxi = wave_min_pk16(ok ? ((0xFFFFu - ttx) | ((0xFFFFu - tty) << 16)) : 0xFFFFFFFFu);
         ushort4 rec = empty_box();
-        if (mxx >= 0) {
-            const int t0x = wave_min(ok ? tx[k] : 0x7FFFFFFF) / TW, t1x = mxx / TW;
-            const int t0y = wave_min(ok ? ty[k] : 0x7FFFFFFF) / TH, t1y = wave_max(ok ? ty[k] : -1) / TH;
+        if ((mn & 0xFFFFu) != 0xFFFFu) {
+            const int t0x = int(mn & 0xFFFFu), t0y = int(mn >> 16);
+            const int t1x = int(0xFFFFu - (mxi & 0xFFFFu)), t1y = int(0xFFFFu - (mxi >> 16));
             if ((t1x - t0x + 1) * (t1y - t0y + 1) > MAX_TILES_PER_BLOCK) {
                 // non-smooth flow: this block's sources go through the key slab
                 const int i = sbx * SBW + (lane % SBW);
                 const int64_t p = int64_t(j) * W + i;
                 const unsigned long long key = ok ? make_key(depth[b * HW + p], unsigned(p)) : 0ull;
                 wave_run_atomic_min(ws.keys + int64_t(bl) * HW, ok ? ty[k] * W + tx[k] : -1, key);
-                if (ok) ws.flag[int64_t(bl) * g.ntiles + (ty[k] / TH) * g.tilesX + tx[k] / TW] = 0u;
+                if (ok) ws.flag[int64_t(bl) * g.ntiles + int(tty) * g.tilesX + int(ttx)] = 0u;
             } else {
                 rec = make_ushort4((unsigned short)t0x, (unsigned short)t1x, (unsigned short)t0y,
                                    (unsigned short)t1y);
@@ -351,16 +361,26 @@ __device__ __forceinline__ void bin_role(int wg, const Coords &co, const float *
                                                 (unsigned short)s1y);
 }
 
-// ---- TILE role
+// ---- SPLAT.  Workgroup id -> XCD-aware tile: dispatch is round-robin over the
+// 8 XCDs (workgroups b and b+8 share one), so each XCD gets a contiguous run
+// of tiles -- neighbouring tiles share source blocks and box records in its
+// L2.  Placement only affects speed, never results.
 template <typename Coords, bool kStamp = false>
-__device__ __forceinline__ void tile_role(TileLds &L, int lin, const Coords &co, const float *__restrict__ obj,
-                                          const float *__restrict__ depth, float *__restrict__ out,
-                                          float *__restrict__ valid, float *__restrict__ coll,
-                                          const ChunkArgs &a, int C, int H, int W, int64_t HW,
-                                          const TileGeom &g, unsigned long long *ph = nullptr) {
+__global__ __launch_bounds__(kWarpThreads, 8) void splat_kernel(Coords co, const float *__restrict__ depth,
+                                                                float *__restrict__ valid, float *__restrict__ coll,
+                                                                ChunkArgs a, int H, int W, int64_t HW, TileGeom g,
+                                                                unsigned long long *stamps = nullptr) {
+    __shared__ TileLds L;
+    const unsigned total = unsigned(a.nimg) * unsigned(g.ntiles);
+    const unsigned per = (total + 7u) / 8u;
+    const unsigned lin = (blockIdx.x % 8u) * per + blockIdx.x / 8u;
+    if (lin >= total) return;
+    unsigned long long *ph = kStamp ? stamps + 8 * lin : nullptr;
+    if constexpr (kStamp) { if (threadIdx.x == 0) ph[0] = wall_clock64(); }
+
     const Ws &ws = a.ws;
-    const int bl = lin / g.ntiles;
-    const int tile = lin - bl * g.ntiles;
+    const int bl = int(lin / unsigned(g.ntiles));
+    const int tile = int(lin - unsigned(bl) * unsigned(g.ntiles));
     const int tyi = tile / g.tilesX, txi = tile - tyi * g.tilesX;
     const int x0 = txi * TW, y0 = tyi * TH;
     const int64_t b = a.b0 + bl;
@@ -400,6 +420,7 @@ __device__ __forceinline__ void tile_role(TileLds &L, int lin, const Coords &co,
     // image if too many segments matched
     const bool all_blocks = nsel > kSegCap;
     const int ncand = all_blocks ? g.nsb : nsel * SEGB;
+    const int lane = lane_id(), wave = threadIdx.x >> 6;
 
     for (int c0 = 0; c0 < ncand; c0 += kListCap) {
         // ---- 2. candidate blocks whose box holds this tile -> L.blk
@@ -426,7 +447,6 @@ __device__ __forceinline__ void tile_role(TileLds &L, int lin, const Coords &co,
         // source block (block id wave-uniform, pixel = lane), kSplatU blocks in
         // flight per wave: every lane holds 3*kSplatU loads at once.
         const int nb = int(L.nblk);
-        const int lane = lane_id(), wave = threadIdx.x >> 6;
         for (int e0 = wave; e0 < nb; e0 += kWaves * kSplatU) {
             typename Coords::V cx[kSplatU], cy[kSplatU];
             float d[kSplatU];
@@ -466,7 +486,7 @@ __device__ __forceinline__ void tile_role(TileLds &L, int lin, const Coords &co,
         __syncthreads();
     }
     if constexpr (kStamp) { if (threadIdx.x == 0) ph[5] = wall_clock64(); }
-    // ---- 4. merge the key slab where the BIN role spilled into it
+    // ---- 4. merge the key slab where BIN spilled into it
     if (L.flag == 0u) {
         for (int k = threadIdx.x; k < TW * TH; k += kWarpThreads) {
             const int ly = k / TW, lx = k - ly * TW;
@@ -482,101 +502,56 @@ __device__ __forceinline__ void tile_role(TileLds &L, int lin, const Coords &co,
         }
         __syncthreads();
     }
-
     if constexpr (kStamp) { if (threadIdx.x == 0) { ph[6] = wall_clock64(); ph[7] = L.nseg; } }
-    // ---- 5. resolve.  Lane-strided: a wave covers 64 consecutive targets of
-    // one tile row, so every gather / store wave-instruction spans one
-    // contiguous row segment.  A thread owns kPer targets, handled kHalf at a
-    // time with all gathers of up to kChan channels in flight before any store.
-    // Offsets are 32-bit from the image base (C*H*W < 2^30 checked on the host).
-    constexpr int kPer = TW * TH / kWarpThreads;  // 8
-    constexpr int kHalf = 4;
-    constexpr int kChan = 4;
-    const float *ob = obj + b * C * HW;
-    float *oo = out + b * C * HW;
+    // ---- 5. publish: winner index, valid, collision (lane-consecutive rows)
+    unsigned int *win = ws.winner + int64_t(bl) * HW;
     float *vb = valid + b * HW;
     float *cb = coll + b * HW;
-    const unsigned uHW = unsigned(HW);
 #pragma unroll
-    for (int h = 0; h < kPer; h += kHalf) {
-        int src[kHalf];
-        unsigned t[kHalf];
-        bool live[kHalf];
-#pragma unroll
-        for (int k = 0; k < kHalf; ++k) {
-            const int q = int(threadIdx.x) + (h + k) * kWarpThreads;
-            const int ly = q / TW, lx = q - ly * TW;
-            const int ty = y0 + ly, tx = x0 + lx;
-            live[k] = ty < H && tx < W;
-            t[k] = unsigned(ty) * unsigned(W) + unsigned(tx);
-            const unsigned long long key = L.zk[q];
-            const bool touched = key != KEY_UNTOUCHED;
-            const bool nowin = key == KEY_NOWIN;
-            src[k] = (touched && !nowin) ? int(key & 0xFFFFFFFFull) : -1;
-            if (live[k]) {
-                vb[t[k]] = touched ? 1.f : 0.f;
-                cb[t[k]] = nowin ? 1.f : 0.f;
-            }
-        }
-        for (int c0 = 0; c0 < C; c0 += kChan) {
-            float o[kChan][kHalf];
-#pragma unroll
-            for (int cc = 0; cc < kChan; ++cc) {
-                const bool chan = c0 + cc < C;
-                const unsigned pl = unsigned(c0 + cc) * uHW;
-#pragma unroll
-                for (int k = 0; k < kHalf; ++k)
-                    o[cc][k] = (chan && src[k] >= 0) ? ob[pl + unsigned(src[k])] : 0.f;
-            }
-#pragma unroll
-            for (int cc = 0; cc < kChan; ++cc) {
-                if (c0 + cc >= C) break;
-                float *dst = oo + unsigned(c0 + cc) * uHW;
-#pragma unroll
-                for (int k = 0; k < kHalf; ++k)
-                    if (live[k]) dst[t[k]] = o[cc][k];
-            }
-        }
-    }
-}
-
-// The fused launch.  Workgroup id -> (XCD-aware) slot x; slots are dealt to
-// the BIN role at an even stride among the TILE slots.  Dispatch is round-robin
-// over the 8 XCDs (workgroups b and b+8 share one), so slot x = contiguous runs
-// per XCD keeps neighbouring tiles -- which share source blocks and gather
-// rows -- in one L2.  Placement only affects speed, never results.
-template <typename Coords, bool kStamp = false>
-__global__ __launch_bounds__(kWarpThreads, 8) void warp_kernel(Coords co, const float *__restrict__ obj,
-                                                               const float *__restrict__ depth,
-                                                               float *__restrict__ out, float *__restrict__ valid,
-                                                               float *__restrict__ coll, ChunkArgs tile_a,
-                                                               ChunkArgs bin_a, int C, int H, int W, int64_t HW,
-                                                               TileGeom g, unsigned long long *stamps = nullptr) {
-    __shared__ WarpLds lds;
-    const unsigned N = unsigned(tile_a.nwg + bin_a.nwg);
-    const unsigned per = (N + 7u) / 8u;
-    const unsigned x = (blockIdx.x % 8u) * per + blockIdx.x / 8u;
-    if (x >= N) return;
-    unsigned long long t_start = 0;
-    if constexpr (kStamp) t_start = wall_clock64();  // diagnostic build only (tools/probe_tile)
-    // number of BIN slots among [0, x) at an even stride
-    const unsigned nb0 = unsigned((uint64_t(x) * unsigned(bin_a.nwg)) / N);
-    const unsigned nb1 = unsigned((uint64_t(x + 1) * unsigned(bin_a.nwg)) / N);
-    const bool is_bin = nb1 > nb0;
-    if (is_bin) {
-        bin_role<Coords>(int(nb0), co, depth, bin_a, H, W, HW, g);
-    } else {
-        tile_role<Coords, kStamp>(lds.tile, int(x - nb0), co, obj, depth, out, valid, coll, tile_a, C, H, W, HW, g,
-                                  kStamp ? stamps + 8 * x : nullptr);
+    for (int k = 0; k < TW * TH / kWarpThreads; ++k) {
+        const int q = int(threadIdx.x) + k * kWarpThreads;
+        const int ly = q / TW, lx = q - ly * TW;
+        const int ty = y0 + ly, tx = x0 + lx;
+        if (ty >= H || tx >= W) continue;
+        const unsigned long long key = L.zk[q];
+        const bool touched = key != KEY_UNTOUCHED;
+        const bool nowin = key == KEY_NOWIN;
+        const unsigned t = unsigned(ty) * unsigned(W) + unsigned(tx);
+        win[t] = (touched && !nowin) ? unsigned(key & 0xFFFFFFFFull) : WIN_NONE;
+        vb[t] = touched ? 1.f : 0.f;
+        cb[t] = nowin ? 1.f : 0.f;
     }
     if constexpr (kStamp) {
         __syncthreads();
-        if (threadIdx.x == 0) {
-            stamps[8 * x + 0] = t_start;
-            stamps[8 * x + 1] = wall_clock64();
-            stamps[8 * x + 2] = is_bin ? 1 : 0;
-            stamps[8 * x + 3] = is_bin ? nb0 : x - nb0;
-        }
+        if (threadIdx.x == 0) { ph[1] = wall_clock64(); ph[2] = 0; ph[3] = lin; }
+    }
+}
+
+// ---- RESOLVE: one target per thread, grid (pixel blocks, images) so no
+// division is needed; 32-bit offsets inside an image (C*H*W < 2^30 is checked
+// on the host).  The gathers of up to kChan channels are in flight before the
+// stores.
+template <int kChan>
+__global__ __launch_bounds__(kResolveThreads) void resolve_kernel(const float *__restrict__ obj,
+                                                                  const unsigned int *__restrict__ winner,
+                                                                  float *__restrict__ out, int C, int64_t HW,
+                                                                  int64_t b0) {
+    const unsigned p = blockIdx.x * kResolveThreads + threadIdx.x;
+    if (p >= unsigned(HW)) return;
+    const int64_t bl = blockIdx.y, b = b0 + bl;
+    const unsigned w = winner[bl * HW + p];
+    const float *ob = obj + b * C * HW;
+    float *oo = out + b * C * HW;
+    const unsigned uHW = unsigned(HW);
+    const bool win = w != WIN_NONE;
+    for (int c0 = 0; c0 < C; c0 += kChan) {
+        float o[kChan];
+#pragma unroll
+        for (int cc = 0; cc < kChan; ++cc)
+            o[cc] = (win && c0 + cc < C) ? ob[unsigned(c0 + cc) * uHW + w] : 0.f;
+#pragma unroll
+        for (int cc = 0; cc < kChan; ++cc)
+            if (c0 + cc < C) oo[unsigned(c0 + cc) * uHW + p] = o[cc];
     }
 }
 
@@ -772,61 +747,43 @@ int run_f32(Coords co, const float *obj, const float *depth, float *out, float *
     // the tile engine's gathers use 32-bit offsets inside one image
     const Mode mode = (C * HW < (int64_t(1) << 30)) ? engine_mode() : Mode::Atomic;
 
-    // Slab layout (shared by both engines so the all-ones key / flag regions
-    // are the same bytes whichever engine ran last): two slabs when they fit,
-    // chunk c in slab c % 2; otherwise one slab.
-    int64_t G = chunk_images(B, HW, per_image, ws_bytes / 2);
-    int nslab = 2;
-    if (G < 1 || G >= B) {
-        G = chunk_images(B, HW, per_image, ws_bytes);
-        nslab = 1;
-    }
+    // One slab of G images, shared by both engines (so the all-ones key /
+    // flag regions are the same bytes whichever engine ran last).  Chunks are
+    // large: every kernel's grid is then many times the resident slots, which
+    // measured best (a two-stream pipeline of small, cache-resident chunks
+    // lost: ~10 us per cross-stream event hop, and the latency-bound BIN ran
+    // 3-4x slower beside a streaming RESOLVE).
+    const int64_t G = chunk_images(B, HW, per_image, ws_bytes);
     if (G < 1) return OFD_FW_EWORKSPACE;
     const int64_t nch = (B + G - 1) / G;
-    if (claim_layout(ws, LayoutSig{H, W, G, nslab})) {
-        const hipError_t e = hipMemsetAsync(ws, 0xFF, size_t(nslab) * size_t(G) * per_image, st);
+    if (claim_layout(ws, LayoutSig{H, W, G, 1})) {
+        const hipError_t e = hipMemsetAsync(ws, 0xFF, size_t(G) * per_image, st);
         if (e != hipSuccess) return int(e);
     }
-    Ws slab[2];
-    slab[0] = carve(ws, G, HW, g);
-    slab[1] = carve(static_cast<char *>(ws) + size_t(G) * per_image, G, HW, g);
-
-    if (mode == Mode::Atomic) {
-        for (int64_t c = 0; c < nch; ++c) {
-            const int64_t b0 = c * G;
-            const int64_t nb = (B - b0) < G ? (B - b0) : G;
-            const int64_t px = nb * HW;
-            unsigned long long *keys = slab[nslab == 2 ? c % 2 : 0].keys;
+    const Ws slab = carve(ws, G, HW, g);
+    for (int64_t c = 0; c < nch; ++c) {
+        const int64_t b0 = c * G;
+        const int64_t nb = (B - b0) < G ? (B - b0) : G;
+        const int64_t px = nb * HW;
+        if (mode == Mode::Atomic) {
             hipLaunchKernelGGL((splat_atomic_kernel<Coords>), dim3(grid_for(px, kBlock * 4)), dim3(kBlock), 0, st,
-                               co, depth, keys, int(H), int(W), HW, b0, px);
+                               co, depth, slab.keys, int(H), int(W), HW, b0, px);
             hipLaunchKernelGGL(resolve_atomic_kernel, dim3(grid_for(px, kBlock * 4)), dim3(kBlock), 0, st,
-                               obj, keys, out, valid, coll, int(C), HW, b0, px);
-        }
-    } else {
-        // launch L runs TILE(chunk L-1) beside BIN(chunk L); with one slab the
-        // BIN and TILE launches alternate.
-        auto chunk = [&](int64_t c, int role_bin) {
-            ChunkArgs a;
-            a.ws = slab[nslab == 2 ? c % 2 : 0];
-            a.b0 = c * G;
-            a.nimg = int((B - a.b0) < G ? (B - a.b0) : G);
-            a.nwg = role_bin ? int((int64_t(a.nimg) * g.nseg + kWaves - 1) / kWaves) : a.nimg * g.ntiles;
-            return a;
-        };
-        ChunkArgs none{};
-        auto launch = [&](const ChunkArgs &t, const ChunkArgs &b) {
-            const unsigned N = unsigned(t.nwg + b.nwg);
-            hipLaunchKernelGGL((warp_kernel<Coords>), dim3((N + 7u) / 8u * 8u), dim3(kWarpThreads), 0, st,
-                               co, obj, depth, out, valid, coll, t, b, int(C), int(H), int(W), HW, g);
-        };
-        if (nslab == 2) {
-            for (int64_t L = 0; L <= nch; ++L)
-                launch(L >= 1 ? chunk(L - 1, 0) : none, L < nch ? chunk(L, 1) : none);
+                               obj, slab.keys, out, valid, coll, int(C), HW, b0, px);
         } else {
-            for (int64_t c = 0; c < nch; ++c) {
-                launch(none, chunk(c, 1));
-                launch(chunk(c, 0), none);
-            }
+            const ChunkArgs a{slab, b0, int(nb)};
+            hipLaunchKernelGGL((bin_kernel<Coords>), dim3(grid_for(nb * g.nseg, kWaves)), dim3(kWarpThreads), 0, st,
+                               co, depth, a, int(H), int(W), HW, g);
+            const unsigned tiles = unsigned(nb * g.ntiles);
+            hipLaunchKernelGGL((splat_kernel<Coords>), dim3((tiles + 7u) / 8u * 8u), dim3(kWarpThreads), 0, st,
+                               co, depth, valid, coll, a, int(H), int(W), HW, g, nullptr);
+            const dim3 rgrid(grid_for(HW, kResolveThreads), unsigned(nb));
+            if (C <= 8)
+                hipLaunchKernelGGL(resolve_kernel<8>, rgrid, dim3(kResolveThreads), 0, st, obj, slab.winner, out,
+                                   int(C), HW, b0);
+            else
+                hipLaunchKernelGGL(resolve_kernel<4>, rgrid, dim3(kResolveThreads), 0, st, obj, slab.winner, out,
+                                   int(C), HW, b0);
         }
     }
     const hipError_t e = hipGetLastError();
@@ -865,8 +822,8 @@ size_t ofd_fw_workspace_bytes(int64_t B, int64_t H, int64_t W, int f64) {
     size_t g = kDefaultChunkPixels / (size_t(H) * size_t(W));
     if (const char *e = getenv("OFD_FW_CHUNK_IMAGES")) g = size_t(atoi(e));
     if (g < 1) g = 1;
-    if (g >= size_t(B)) return size_t(B) * per_image;  // one chunk, one slab
-    return 2 * g * per_image;                          // double-buffered slabs
+    if (g > size_t(B)) g = size_t(B);
+    return g * per_image;
 }
 
 int ofd_fw_workspace_init(void *workspace, size_t bytes, void *stream) {

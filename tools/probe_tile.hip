@@ -1,29 +1,32 @@
 // tools/probe_tile.hip -- diagnostic build of the TILE engine (not shipped).
 // Same translation unit as the product (#include), with per-workgroup wall
-// clock stamps (warp_kernel<..., kStamp = true>) so a Python driver can see
-// each role's workgroup latency distribution and the launch spans.
+// clock stamps in the SPLAT kernel (splat_kernel<..., kStamp = true>) so a
+// Python driver can time BIN / SPLAT / RESOLVE separately and see the SPLAT
+// workgroups' phase split.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Iinclude \
 //         -o tools/_build/libprobe_tile.so tools/probe_tile.hip
 #include "../opticalflowfromdepth_amd/csrc/ofd_fw.hip"
 
-extern "C" int probe_launch(const float *obj, const float *flow, const float *depth, float *out, float *valid,
-                            float *coll, int64_t C, int64_t H, int64_t W, void *slab, int64_t tile_b0,
-                            int tile_nimg, int64_t bin_b0, int bin_nimg, int G, unsigned long long *stamps,
-                            void *stream) {
+// which: 0 = BIN, 1 = SPLAT (stamped), 2 = RESOLVE
+extern "C" int probe_launch(int which, const float *obj, const float *flow, const float *depth, float *out,
+                            float *valid, float *coll, int64_t C, int64_t H, int64_t W, void *slab, int64_t b0,
+                            int nimg, unsigned long long *stamps, void *stream) {
     const int64_t HW = H * W;
     const TileGeom g = make_geom(H, W);
     FlowCoords<float> co{flow, HW};
-    ChunkArgs t{}, b{};
-    Ws w = carve(slab, G, HW, g);
-    if (tile_nimg > 0) { t.ws = w; t.b0 = tile_b0; t.nimg = tile_nimg; t.nwg = tile_nimg * g.ntiles; }
-    if (bin_nimg > 0) {
-        b.ws = w; b.b0 = bin_b0; b.nimg = bin_nimg;
-        b.nwg = int((int64_t(bin_nimg) * g.nseg + kWaves - 1) / kWaves);
+    const ChunkArgs a{carve(slab, nimg, HW, g), b0, nimg};
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (which == 0) {
+        hipLaunchKernelGGL((bin_kernel<FlowCoords<float>>), dim3(grid_for(int64_t(nimg) * g.nseg, kWaves)),
+                           dim3(kWarpThreads), 0, st, co, depth, a, int(H), int(W), HW, g);
+    } else if (which == 1) {
+        const unsigned tiles = unsigned(nimg * g.ntiles);
+        hipLaunchKernelGGL((splat_kernel<FlowCoords<float>, true>), dim3((tiles + 7u) / 8u * 8u),
+                           dim3(kWarpThreads), 0, st, co, depth, valid, coll, a, int(H), int(W), HW, g, stamps);
+    } else {
+        hipLaunchKernelGGL(resolve_kernel<8>, dim3(grid_for(HW, kResolveThreads), unsigned(nimg)),
+                           dim3(kResolveThreads), 0, st, obj, a.ws.winner, out, int(C), HW, b0);
     }
-    const unsigned N = unsigned(t.nwg + b.nwg);
-    hipLaunchKernelGGL((warp_kernel<FlowCoords<float>, true>), dim3((N + 7u) / 8u * 8u), dim3(kWarpThreads), 0,
-                       static_cast<hipStream_t>(stream), co, obj, depth, out, valid, coll, t, b, int(C), int(H),
-                       int(W), HW, g, stamps);
     return int(hipGetLastError());
 }
 
