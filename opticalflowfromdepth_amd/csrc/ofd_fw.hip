@@ -152,24 +152,11 @@ struct FlowCoords {  // FW.forward input: flow [B,2,H,W], ch0 = x, ch1 = y
 // ---------------------------------------------------------------- wave helpers
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
-// Wave-wide min of two packed unsigned 16-bit values (v_pk_min_u16) with DPP
-// row operations (no LDS round trip): quad swaps and row mirrors reduce each
-// 16-lane row, then row_bcast:15 / row_bcast:31 fold the four rows into lane
-// 63, which readlane broadcasts.  One reduction yields (min lo, min hi).
+// Packed min of two unsigned 16-bit halves (one v_pk_min_u16).
 __device__ __forceinline__ unsigned pk_min_u16(unsigned a, unsigned b) {
     unsigned r;
     asm volatile("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
     return r;
-}
-__device__ __forceinline__ unsigned wave_min_pk16(unsigned v) {
-    constexpr int ident = -1;  // 0xFFFF in both halves
-    v = pk_min_u16(v, unsigned(__builtin_amdgcn_update_dpp(ident, int(v), 0xB1, 0xF, 0xF, false)));
-    v = pk_min_u16(v, unsigned(__builtin_amdgcn_update_dpp(ident, int(v), 0x4E, 0xF, 0xF, false)));
-    v = pk_min_u16(v, unsigned(__builtin_amdgcn_update_dpp(ident, int(v), 0x141, 0xF, 0xF, false)));
-    v = pk_min_u16(v, unsigned(__builtin_amdgcn_update_dpp(ident, int(v), 0x140, 0xF, 0xF, false)));
-    v = pk_min_u16(v, unsigned(__builtin_amdgcn_update_dpp(ident, int(v), 0x142, 0xA, 0xF, false)));
-    v = pk_min_u16(v, unsigned(__builtin_amdgcn_update_dpp(ident, int(v), 0x143, 0xC, 0xF, false)));
-    return unsigned(__builtin_amdgcn_readlane(int(v), 63));
 }
 
 // Global atomic min of `key` into base[t] for every lane with t >= 0, issuing
@@ -299,6 +286,20 @@ struct ChunkArgs {  // one chunk of images
 };
 
 // ---- BIN: wave w of workgroup blockIdx.x boxes segment blockIdx.x * kWaves + w.
+// A segment is 128 x 4 px (SEGB = 8 blocks of 16 x 4).  Load instruction
+// (row r, half h) covers 64 contiguous pixels of one row (256 B per plane), so
+// lane l of half h belongs to block h*4 + l/16.  A lane first folds its 4 rows
+// in registers; then a row-local DPP reduction (16-lane DPP rows = one block's
+// columns) gives every lane its block's tile box.
+__device__ __forceinline__ unsigned row16_min_pk16(unsigned v) {
+    constexpr int ident = -1;
+    v = pk_min_u16(v, unsigned(__builtin_amdgcn_update_dpp(ident, int(v), 0xB1, 0xF, 0xF, false)));   // quad [1,0,3,2]
+    v = pk_min_u16(v, unsigned(__builtin_amdgcn_update_dpp(ident, int(v), 0x4E, 0xF, 0xF, false)));   // quad [2,3,0,1]
+    v = pk_min_u16(v, unsigned(__builtin_amdgcn_update_dpp(ident, int(v), 0x141, 0xF, 0xF, false)));  // row_half_mirror
+    v = pk_min_u16(v, unsigned(__builtin_amdgcn_update_dpp(ident, int(v), 0x140, 0xF, 0xF, false)));  // row_mirror
+    return v;
+}
+
 template <typename Coords>
 __global__ __launch_bounds__(kWarpThreads) void bin_kernel(Coords co, const float *__restrict__ depth, ChunkArgs a,
                                                            int H, int W, int64_t HW, TileGeom g) {
@@ -310,40 +311,59 @@ __global__ __launch_bounds__(kWarpThreads) void bin_kernel(Coords co, const floa
     const int sg = int(sgg - int64_t(bl) * g.nseg);
     const int sby = sg / g.nsegx, sgx = sg - sby * g.nsegx;
     const int64_t b = a.b0 + bl;
-    const int j = sby * SBH + (lane / SBW);
-    int tx[SEGB], ty[SEGB];
+    int tx[2][SBH], ty[2][SBH];
 #pragma unroll
-    for (int k = 0; k < SEGB; ++k) {
-        const int i = (sgx * SEGB + k) * SBW + (lane % SBW);
-        tx[k] = ty[k] = -1;
-        if (i < W && j < H) {
-            typename Coords::V x, y;
-            co.load(b, int64_t(j) * W + i, x, y);
-            co.target(i, j, x, y, H, W, tx[k], ty[k]);
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int r = 0; r < SBH; ++r) {
+            const int i = sgx * (SEGB * SBW) + h * 64 + lane, j = sby * SBH + r;
+            tx[h][r] = ty[h][r] = -1;
+            if (i < W && j < H) {
+                typename Coords::V x, y;
+                co.load(b, int64_t(j) * W + i, x, y);
+                co.target(i, j, x, y, H, W, tx[h][r], ty[h][r]);
+            }
         }
+    // per lane: packed (tile x, tile y) min and (0xFFFF - tile x, 0xFFFF - tile y) min
+    unsigned mn[2], mxi[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        unsigned m = 0xFFFFFFFFu, x = 0xFFFFFFFFu;
+#pragma unroll
+        for (int r = 0; r < SBH; ++r) {
+            if (tx[h][r] >= 0) {
+                const unsigned ttx = unsigned(tx[h][r] / TW), tty = unsigned(ty[h][r] / TH);
+                m = pk_min_u16(m, ttx | (tty << 16));
+                x = pk_min_u16(x, (0xFFFFu - ttx) | ((0xFFFFu - tty) << 16));
+            }
+        }
+        mn[h] = row16_min_pk16(m);
+        mxi[h] = row16_min_pk16(x);
     }
     int s0x = 0x7FFFFFFF, s1x = -1, s0y = 0x7FFFFFFF, s1y = -1;
 #pragma unroll
     for (int k = 0; k < SEGB; ++k) {
         const int sbx = sgx * SEGB + k;
         if (sbx >= g.nsbx) break;  // wave-uniform
-        const bool ok = tx[k] >= 0;
-        // tile-unit box: min over (tile x, tile y) and over (0xFFFF - tile x,
-        // 0xFFFF - tile y), two packed 16-bit reductions
-        const unsigned ttx = ok ? unsigned(tx[k] / TW) : 0xFFFFu, tty = ok ? unsigned(ty[k] / TH) : 0xFFFFu;
-        const unsigned mn = wave_min_pk16(ttx | (tty << 16));
-        const unsigned mxi = wave_min_pk16(ok ? ((0xFFFFu - ttx) | ((0xFFFFu - tty) << 16)) : 0xFFFFFFFFu);
+        const int h = k / 4, src_lane = (k % 4) * 16;
+        const unsigned bmn = unsigned(__builtin_amdgcn_readlane(int(mn[h]), src_lane));
+        const unsigned bmx = unsigned(__builtin_amdgcn_readlane(int(mxi[h]), src_lane));
         ushort4 rec = empty_box();
-        if ((mn & 0xFFFFu) != 0xFFFFu) {
-            const int t0x = int(mn & 0xFFFFu), t0y = int(mn >> 16);
-            const int t1x = int(0xFFFFu - (mxi & 0xFFFFu)), t1y = int(0xFFFFu - (mxi >> 16));
+        if ((bmn & 0xFFFFu) != 0xFFFFu) {
+            const int t0x = int(bmn & 0xFFFFu), t0y = int(bmn >> 16);
+            const int t1x = int(0xFFFFu - (bmx & 0xFFFFu)), t1y = int(0xFFFFu - (bmx >> 16));
             if ((t1x - t0x + 1) * (t1y - t0y + 1) > MAX_TILES_PER_BLOCK) {
                 // non-smooth flow: this block's sources go through the key slab
-                const int i = sbx * SBW + (lane % SBW);
-                const int64_t p = int64_t(j) * W + i;
-                const unsigned long long key = ok ? make_key(depth[b * HW + p], unsigned(p)) : 0ull;
-                wave_run_atomic_min(ws.keys + int64_t(bl) * HW, ok ? ty[k] * W + tx[k] : -1, key);
-                if (ok) ws.flag[int64_t(bl) * g.ntiles + int(tty) * g.tilesX + int(ttx)] = 0u;
+                const bool mine_lane = (lane >> 4) == (k % 4);
+#pragma unroll
+                for (int r = 0; r < SBH; ++r) {
+                    const bool ok = mine_lane && tx[h][r] >= 0;
+                    const int i = sgx * (SEGB * SBW) + h * 64 + lane, j = sby * SBH + r;
+                    const int64_t p = int64_t(j) * W + i;
+                    const unsigned long long key = ok ? make_key(depth[b * HW + p], unsigned(p)) : 0ull;
+                    wave_run_atomic_min(ws.keys + int64_t(bl) * HW, ok ? ty[h][r] * W + tx[h][r] : -1, key);
+                    if (ok) ws.flag[int64_t(bl) * g.ntiles + (ty[h][r] / TH) * g.tilesX + tx[h][r] / TW] = 0u;
+                }
             } else {
                 rec = make_ushort4((unsigned short)t0x, (unsigned short)t1x, (unsigned short)t0y,
                                    (unsigned short)t1y);

@@ -76,6 +76,5 @@ def main():
     ok = all(torch.equal(x, y) for x, y in zip((out, valid, coll), ref))
     print("probe result == product result:", ok)
 
-
 if __name__ == "__main__":
     main()
