@@ -115,13 +115,20 @@ def main():
         print(f"# check vs oracle (image 0): {'OK' if ok else 'MISMATCH'}", file=sys.stderr)
 
     stream = torch.cuda.current_stream(dev)
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    mk = lambda: [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    starts, ends, rstarts, rends = mk(), mk(), mk(), mk()
+    for ev in rstarts + rends:  # torch creates events lazily: force the HIP handles to exist
+        ev.record(stream)
+    torch.cuda.synchronize()
+    lib = _native.lib()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
+        # events around the dominant kernel (RESOLVE), recorded by the library
+        # on the launch stream (include/ofd_fw.h: ofd_fw_set_profile_events)
+        lib.ofd_fw_set_profile_events(rstarts[k].cuda_event, rends[k].cuda_event)
         starts[k].record(stream)
         forward_warp_flow(obj, flow, depth, out=out)
         ends[k].record(stream)
@@ -129,8 +136,11 @@ def main():
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
+    lib.ofd_fw_set_profile_events(None, None)
     ev_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
     dev_ms = sum(ev_ms) / len(ev_ms)
+    rv_ms = [s.elapsed_time(e) for s, e in zip(rstarts, rends)]
+    resolve_ms = sum(rv_ms) / len(rv_ms)
 
     t = torch.tensor([wall, dev_ms], dtype=torch.float64, device=dev)
     if world > 1:
@@ -141,15 +151,23 @@ def main():
     bytes_per_px = (2 * C + 5) * 4  # algorithmic: obj C + flow 2 + depth in; out C + valid + coll
     value = n_total * H * W * args.steps / wall / 1e6
     achieved_gbs = px_step_rank * bytes_per_px / (dev_ms / 1e3) / 1e9
+    # dominant kernel: RESOLVE (tile engine) gathers obj and writes the C output
+    # planes; the atomic engine's resolve pass also writes valid / collision
+    kern_bpp = (2 * C) * 4 if args.engine == "tile" else (2 * C + 2) * 4
+    kern_name = "resolve_kernel" if args.engine == "tile" else "resolve_atomic_kernel"
+    kern_gbs = px_step_rank * kern_bpp / (resolve_ms / 1e3) / 1e9
 
-    traffic = None
+    traffic = traffic_step = None
     traffic_note = None
     pmc_file = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc_file):
+    if os.path.exists(pmc_file) and args.engine == "tile":
         try:
             pm = json.load(open(pmc_file))
             if pm.get("config") == [B, C, H, W]:
-                traffic = pm.get("hbm_bytes_per_step")
+                traffic_step = pm.get("hbm_bytes_per_step")
+                for kk in pm.get("kernels", []):
+                    if kk["kernel"] == kern_name:
+                        traffic = kk["fetch_bytes_x2"] + kk["write_bytes"]
                 traffic_note = pm.get("source")
         except Exception:
             pass
@@ -176,13 +194,19 @@ def main():
                                    f"(BASELINE config 3/4)", "global_batch": n_total, "height": H,
                        "width": W, "channels": C, "ego_fraction": args.ego_fraction,
                        "parallelism": f"shard{world} (images, no data-path collective)"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
+            "roofline": {"bound": "hbm", "achieved": round(kern_gbs, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(kern_gbs / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
-                         "kernel": f"ofd_fw forward_warp_flow, {args.engine} engine (all launches of one call)",
-                         "algorithmic_bytes_per_px": bytes_per_px,
-                         "event_ms_per_call": round(dev_ms, 4),
+                         "kernel": f"{kern_name} ({args.engine} engine), dominant kernel of the call",
+                         "algorithmic_bytes_per_px": kern_bpp,
+                         "event_ms_per_launch": round(resolve_ms, 4),
                          "traffic_source": traffic_note},
+            "op_roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS,
+                            "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
+                            "traffic": traffic_step,
+                            "scope": f"whole forward_warp_flow call ({args.engine} engine, all launches)",
+                            "algorithmic_bytes_per_px": bytes_per_px,
+                            "event_ms_per_call": round(dev_ms, 4)},
             "cpu_baseline": cpu,
         }
         print(json.dumps(rec), flush=True)

@@ -68,6 +68,13 @@ int ofd_fw_abi_version(void);
 #define OFD_FW_ENGINE_ATOMIC 1
 int ofd_fw_set_engine(int engine);
 
+/* Benchmark hook: when non-NULL, the given hipEvent_t's are recorded on the
+ * launch stream right before the first and right after the last RESOLVE
+ * launch of each subsequent f32 call (RESOLVE is the dominant kernel; the
+ * ATOMIC engine's resolve pass likewise).  Pass NULLs to disable.  Process-
+ * wide, not thread-safe; for timing only. */
+int ofd_fw_set_profile_events(void *start_event, void *stop_event);
+
 /* Human-readable name of a return code (static storage). */
 const char *ofd_fw_strerror(int code);
 

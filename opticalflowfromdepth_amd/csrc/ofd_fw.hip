@@ -755,6 +755,12 @@ bool claim_layout(const void *ws, const LayoutSig &sig) {
     return !ok;
 }
 
+// Optional timing hook (ofd_fw_set_profile_events): events recorded on the
+// launch stream right before the first and right after the last RESOLVE
+// launch of a call -- the dominant kernel -- so a benchmark can time it with
+// HIP events on the stream it runs on.
+hipEvent_t g_prof_start = nullptr, g_prof_stop = nullptr;
+
 template <typename Coords>
 int run_f32(Coords co, const float *obj, const float *depth, float *out, float *valid, float *coll,
             int64_t B, int64_t C, int64_t H, int64_t W, void *ws, size_t ws_bytes, hipStream_t st) {
@@ -788,8 +794,10 @@ int run_f32(Coords co, const float *obj, const float *depth, float *out, float *
         if (mode == Mode::Atomic) {
             hipLaunchKernelGGL((splat_atomic_kernel<Coords>), dim3(grid_for(px, kBlock * 4)), dim3(kBlock), 0, st,
                                co, depth, slab.keys, int(H), int(W), HW, b0, px);
+            if (c == 0 && g_prof_start) (void)hipEventRecord(g_prof_start, st);
             hipLaunchKernelGGL(resolve_atomic_kernel, dim3(grid_for(px, kBlock * 4)), dim3(kBlock), 0, st,
                                obj, slab.keys, out, valid, coll, int(C), HW, b0, px);
+            if (c == nch - 1 && g_prof_stop) (void)hipEventRecord(g_prof_stop, st);
         } else {
             const ChunkArgs a{slab, b0, int(nb)};
             hipLaunchKernelGGL((bin_kernel<Coords>), dim3(grid_for(nb * g.nseg, kWaves)), dim3(kWarpThreads), 0, st,
@@ -798,12 +806,14 @@ int run_f32(Coords co, const float *obj, const float *depth, float *out, float *
             hipLaunchKernelGGL((splat_kernel<Coords>), dim3((tiles + 7u) / 8u * 8u), dim3(kWarpThreads), 0, st,
                                co, depth, valid, coll, a, int(H), int(W), HW, g, nullptr);
             const dim3 rgrid(grid_for(HW, kResolveThreads), unsigned(nb));
+            if (c == 0 && g_prof_start) (void)hipEventRecord(g_prof_start, st);
             if (C <= 8)
                 hipLaunchKernelGGL(resolve_kernel<8>, rgrid, dim3(kResolveThreads), 0, st, obj, slab.winner, out,
                                    int(C), HW, b0);
             else
                 hipLaunchKernelGGL(resolve_kernel<4>, rgrid, dim3(kResolveThreads), 0, st, obj, slab.winner, out,
                                    int(C), HW, b0);
+            if (c == nch - 1 && g_prof_stop) (void)hipEventRecord(g_prof_stop, st);
         }
     }
     const hipError_t e = hipGetLastError();
@@ -815,6 +825,12 @@ int run_f32(Coords co, const float *obj, const float *depth, float *out, float *
 extern "C" {
 
 int ofd_fw_abi_version(void) { return OFD_FW_ABI_VERSION; }
+
+int ofd_fw_set_profile_events(void *start_event, void *stop_event) {
+    g_prof_start = static_cast<hipEvent_t>(start_event);
+    g_prof_stop = static_cast<hipEvent_t>(stop_event);
+    return OFD_FW_OK;
+}
 
 int ofd_fw_set_engine(int engine) {
     const int prev = int(engine_mode());
