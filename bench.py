@@ -84,10 +84,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # OFD_BENCH_BACKEND=gloo + OFD_BENCH_SAME_DEVICE=1 rehearse the N>1 path on
+    # a one-GPU box (all ranks on cuda:0, CPU collectives); the default is one
+    # rank per GPU with RCCL ("nccl" on ROCm).
+    backend = os.environ.get("OFD_BENCH_BACKEND", "nccl")
+    gpu = 0 if os.environ.get("OFD_BENCH_SAME_DEVICE") == "1" else local
+    dev = torch.device("cuda", gpu)
+    torch.cuda.set_device(dev)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    coll_dev = dev if backend == "nccl" else torch.device("cpu")
 
     from opticalflowfromdepth_amd import forward_warp_flow, shard, synth
     from opticalflowfromdepth_amd import _native
@@ -95,7 +104,7 @@ def main():
     B, H, W = args.batch, args.height, args.width
     n_total = B * world
     seeds = [shard.image_seed(i) for i in range(n_total)]
-    s_all, T_all = shard.broadcast_camera_params(seeds, device=dev)     # RCCL broadcast (setup)
+    s_all, T_all = shard.broadcast_camera_params(seeds, device=coll_dev)  # RCCL broadcast (setup)
     a, b = shard.shard_range(n_total, world, rank)
     obj, flow, depth = synth.stage_one_batch(seeds[a:b], H, W, dev, ego_fraction=args.ego_fraction,
                                              camera=(s_all[a:b], T_all[a:b]))
@@ -142,7 +151,7 @@ def main():
     rv_ms = [s.elapsed_time(e) for s, e in zip(rstarts, rends)]
     resolve_ms = sum(rv_ms) / len(rv_ms)
 
-    t = torch.tensor([wall, dev_ms], dtype=torch.float64, device=dev)
+    t = torch.tensor([wall, dev_ms], dtype=torch.float64, device=coll_dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall, dev_ms_max = float(t[0]), float(t[1])

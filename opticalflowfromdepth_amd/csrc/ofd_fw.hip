@@ -66,7 +66,7 @@ constexpr int TW = 128, TH = 32;          // target tile (LDS z-buffer 32 KiB)
 constexpr int SBW = 16, SBH = 4;          // source block = one wave (64 px)
 constexpr int SEGB = 8;                   // source blocks per segment (128 x 4 px)
 constexpr int MAX_TILES_PER_BLOCK = 12;   // wider boxes go through the global path
-constexpr int kSplatU = 8;                // source blocks in flight per wave (tile role)
+constexpr int kSplatU = 12;               // source blocks in flight per wave (SPLAT)
 
 // Default chunk: 64M source pixels (85 images of 768x1024, a ~830 MB slab).
 // Every kernel of a chunk then has a grid many times the resident slots
@@ -269,7 +269,7 @@ constexpr int kWarpThreads = 512;
 constexpr int kWaves = kWarpThreads / 64;
 constexpr int kSegCap = 768;    // selected segments held in LDS (else: scan all blocks)
 constexpr int kListCap = 1024;  // candidate blocks examined per batch
-constexpr int kResolveThreads = 256;
+constexpr int kResolveRows = 16;  // RESOLVE workgroup = 64 x 16 targets
 constexpr unsigned int WIN_NONE = 0xFFFFFFFFu;
 
 struct TileLds {
@@ -547,18 +547,23 @@ __global__ __launch_bounds__(kWarpThreads, 8) void splat_kernel(Coords co, const
     }
 }
 
-// ---- RESOLVE: one target per thread, grid (pixel blocks, images) so no
-// division is needed; 32-bit offsets inside an image (C*H*W < 2^30 is checked
-// on the host).  The gathers of up to kChan channels are in flight before the
-// stores.
-template <int kChan>
-__global__ __launch_bounds__(kResolveThreads) void resolve_kernel(const float *__restrict__ obj,
-                                                                  const unsigned int *__restrict__ winner,
-                                                                  float *__restrict__ out, int C, int64_t HW,
-                                                                  int64_t b0) {
-    const unsigned p = blockIdx.x * kResolveThreads + threadIdx.x;
-    if (p >= unsigned(HW)) return;
-    const int64_t bl = blockIdx.y, b = b0 + bl;
+// ---- RESOLVE: one target per thread over 2-D target patches -- workgroup =
+// 64 columns x kRows rows (wave = one 64-pixel row segment), grid (x, y,
+// image) so no division is needed.  The gathers of vertically adjacent
+// targets, whose sources share cache lines under rotated / sheared flows, run
+// on one CU at the same time (64x16 measured 5 % faster than 256x1).  32-bit
+// offsets inside an image (C*H*W < 2^30 is checked on the host); the gathers
+// of up to kChan channels are in flight before the stores.
+template <int kChan, int kRows>
+__global__ __launch_bounds__(64 * kRows) void resolve2d_kernel(const float *__restrict__ obj,
+                                                               const unsigned int *__restrict__ winner,
+                                                               float *__restrict__ out, int C, int H, int W,
+                                                               int64_t HW, int64_t b0) {
+    const unsigned x = blockIdx.x * 64u + (threadIdx.x & 63u);
+    const unsigned y = blockIdx.y * unsigned(kRows) + (threadIdx.x >> 6);
+    if (x >= unsigned(W) || y >= unsigned(H)) return;
+    const int64_t bl = blockIdx.z, b = b0 + bl;
+    const unsigned p = y * unsigned(W) + x;
     const unsigned w = winner[bl * HW + p];
     const float *ob = obj + b * C * HW;
     float *oo = out + b * C * HW;
@@ -805,14 +810,15 @@ int run_f32(Coords co, const float *obj, const float *depth, float *out, float *
             const unsigned tiles = unsigned(nb * g.ntiles);
             hipLaunchKernelGGL((splat_kernel<Coords>), dim3((tiles + 7u) / 8u * 8u), dim3(kWarpThreads), 0, st,
                                co, depth, valid, coll, a, int(H), int(W), HW, g, nullptr);
-            const dim3 rgrid(grid_for(HW, kResolveThreads), unsigned(nb));
+            const dim3 rgrid(unsigned((W + 63) / 64), unsigned((H + kResolveRows - 1) / kResolveRows),
+                             unsigned(nb));
             if (c == 0 && g_prof_start) (void)hipEventRecord(g_prof_start, st);
             if (C <= 8)
-                hipLaunchKernelGGL(resolve_kernel<8>, rgrid, dim3(kResolveThreads), 0, st, obj, slab.winner, out,
-                                   int(C), HW, b0);
+                hipLaunchKernelGGL((resolve2d_kernel<8, kResolveRows>), rgrid, dim3(64 * kResolveRows), 0, st, obj,
+                                   slab.winner, out, int(C), int(H), int(W), HW, b0);
             else
-                hipLaunchKernelGGL(resolve_kernel<4>, rgrid, dim3(kResolveThreads), 0, st, obj, slab.winner, out,
-                                   int(C), HW, b0);
+                hipLaunchKernelGGL((resolve2d_kernel<4, kResolveRows>), rgrid, dim3(64 * kResolveRows), 0, st, obj,
+                                   slab.winner, out, int(C), int(H), int(W), HW, b0);
             if (c == nch - 1 && g_prof_stop) (void)hipEventRecord(g_prof_stop, st);
         }
     }

@@ -24,8 +24,9 @@ extern "C" int probe_launch(int which, const float *obj, const float *flow, cons
         hipLaunchKernelGGL((splat_kernel<FlowCoords<float>, true>), dim3((tiles + 7u) / 8u * 8u),
                            dim3(kWarpThreads), 0, st, co, depth, valid, coll, a, int(H), int(W), HW, g, stamps);
     } else {
-        hipLaunchKernelGGL(resolve_kernel<8>, dim3(grid_for(HW, kResolveThreads), unsigned(nimg)),
-                           dim3(kResolveThreads), 0, st, obj, a.ws.winner, out, int(C), HW, b0);
+        hipLaunchKernelGGL((resolve2d_kernel<8, kResolveRows>),
+                           dim3(unsigned((W + 63) / 64), unsigned((H + kResolveRows - 1) / kResolveRows), unsigned(nimg)),
+                           dim3(64 * kResolveRows), 0, st, obj, a.ws.winner, out, int(C), int(H), int(W), HW, b0);
     }
     return int(hipGetLastError());
 }
