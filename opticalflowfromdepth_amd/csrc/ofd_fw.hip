@@ -17,19 +17,22 @@
 //
 //  TILE (default).  Targets are cut into TW x TH tiles whose z-buffer lives in
 //  LDS (ds_min_u64 is ~25x the chip rate of a global 64-bit atomic min,
-//  tools/microbench.hip).  Sources are cut into 64-pixel blocks (one wave).
-//    bin  : one wave per source block computes its targets' bounding box and
-//           appends the block id to the list of every tile the box overlaps
-//           (one global atomic per (block, tile), ~1.4 per block).
-//    tile : one workgroup per target tile re-reads the listed source blocks
-//           (a cache-resident re-read when the batch is processed in chunks),
-//           folds their keys into the LDS z-buffer, then resolves: gathers the
-//           winners' C channels and writes output / valid / collision once,
-//           16-byte stores, no scratch traffic to HBM.
-//    Blocks whose box spans too many tiles (non-smooth flow) and list overflow
-//    (border hot spots) fall back to global atomics on a per-image key slab
-//    (pre-reduced over runs of equal targets inside the wave); the tile kernel
-//    merges that slab for flagged tiles only.
+//  tools/microbench.hip).  Sources are cut into 16 x 4 blocks, 8 blocks to a
+//  128 x 4 segment.  Three kernels per chunk of images:
+//    BIN     : one wave per segment loads its coordinates (16-byte loads),
+//              and writes the tile-space bounding box of every block and of
+//              the segment (8-byte records, no atomics).
+//    SPLAT   : one workgroup per target tile scans the segment boxes, then
+//              the block boxes of the selected segments, re-reads the selected
+//              blocks' coordinates and depths, folds their keys into the LDS
+//              z-buffer and publishes the tile: winner index (u32), valid,
+//              collision.
+//    RESOLVE : one target per thread: reads the winner index, gathers the
+//              winner's C channels and writes them (streaming, HBM-bound).
+//    Blocks whose box spans more than MAX_TILES_PER_BLOCK tiles (non-smooth
+//    flow) go through global atomics on a per-image key slab instead
+//    (pre-reduced over runs of equal targets inside the wave); SPLAT merges
+//    the slab for the tiles BIN flagged.
 //
 //  ATOMIC (OFD_FW_MODE=atomic; and the float64 op).  One global 64-bit atomic
 //  min per source into a per-image key slab, then a resolve pass.
@@ -120,6 +123,23 @@ __device__ __forceinline__ void target_flow(int i, int j, F fx, F fy, int H, int
     ty = int(py);
 }
 
+// Four consecutive pixels p..p+3 (n of them inside the row).  kVec: one
+// 16-byte load per plane (float4, or two double2) -- the caller guarantees
+// 16-byte alignment of every row start (W % 4 == 0, aligned base pointers).
+template <bool kVec, typename T>
+__device__ __forceinline__ void load4(const T *__restrict__ q, T v[4], int n) {
+    if constexpr (kVec && sizeof(T) == 4) {
+        const float4 f = *reinterpret_cast<const float4 *>(q);
+        v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
+    } else if constexpr (kVec) {
+        const double2 f0 = reinterpret_cast<const double2 *>(q)[0], f1 = reinterpret_cast<const double2 *>(q)[1];
+        v[0] = f0.x; v[1] = f0.y; v[2] = f1.x; v[3] = f1.y;
+    } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = e < n ? q[e] : T(0);
+    }
+}
+
 // Coordinate sources: the target of the source at pixel p = j*W + i of image b.
 struct SafeF32 {  // fw_cuda.forward_warping inputs: safe_y, safe_x [B,1,H,W]
     using V = float;
@@ -129,6 +149,12 @@ struct SafeF32 {  // fw_cuda.forward_warping inputs: safe_y, safe_x [B,1,H,W]
         x = sx[b * HW + p];
         y = sy[b * HW + p];
     }
+    template <bool kVec>
+    __device__ __forceinline__ void load4(int64_t b, int64_t p, V x[4], V y[4], int n) const {
+        ::load4<kVec>(sx + b * HW + p, x, n);
+        ::load4<kVec>(sy + b * HW + p, y, n);
+    }
+    __host__ bool vec_ok() const { return (uintptr_t(sx) | uintptr_t(sy)) % 16 == 0; }
     __device__ __forceinline__ void target(int, int, V x, V y, int H, int W, int &tx, int &ty) const {
         target_safe<float>(x, y, H, W, tx, ty);
     }
@@ -144,6 +170,13 @@ struct FlowCoords {  // FW.forward input: flow [B,2,H,W], ch0 = x, ch1 = y
         x = f[0];
         y = f[HW];
     }
+    template <bool kVec>
+    __device__ __forceinline__ void load4(int64_t b, int64_t p, V x[4], V y[4], int n) const {
+        const F *f = flow + b * 2 * HW + p;
+        ::load4<kVec>(f, x, n);
+        ::load4<kVec>(f + HW, y, n);
+    }
+    __host__ bool vec_ok() const { return uintptr_t(flow) % 16 == 0; }
     __device__ __forceinline__ void target(int i, int j, V x, V y, int H, int W, int &tx, int &ty) const {
         target_flow<F>(i, j, x, y, H, W, tx, ty);
     }
@@ -269,7 +302,7 @@ constexpr int kWarpThreads = 512;
 constexpr int kWaves = kWarpThreads / 64;
 constexpr int kSegCap = 768;    // selected segments held in LDS (else: scan all blocks)
 constexpr int kListCap = 1024;  // candidate blocks examined per batch
-constexpr int kResolveRows = 16;  // RESOLVE workgroup = 64 x 16 targets
+constexpr int kResolveWX = 2, kResolveRows = 8;  // RESOLVE workgroup = 128 x 8 targets
 constexpr unsigned int WIN_NONE = 0xFFFFFFFFu;
 
 struct TileLds {
@@ -286,21 +319,21 @@ struct ChunkArgs {  // one chunk of images
 };
 
 // ---- BIN: wave w of workgroup blockIdx.x boxes segment blockIdx.x * kWaves + w.
-// A segment is 128 x 4 px (SEGB = 8 blocks of 16 x 4).  Load instruction
-// (row r, half h) covers 64 contiguous pixels of one row (256 B per plane), so
-// lane l of half h belongs to block h*4 + l/16.  A lane first folds its 4 rows
-// in registers; then a row-local DPP reduction (16-lane DPP rows = one block's
-// columns) gives every lane its block's tile box.
-__device__ __forceinline__ unsigned row16_min_pk16(unsigned v) {
+// A segment is 128 x 4 px (SEGB = 8 blocks of 16 x 4).  Lane l owns the 4
+// consecutive pixels 4*(l%32)..+3 of rows 2q + l/32 (q = 0, 1): one 16-byte
+// load per plane and row pair (kVec), so the segment's coordinates arrive in
+// 4 wave-wide 1 KiB loads instead of 16 of 256 B (dword loads capped BIN at
+// ~3.3 TB/s).  Block k = lanes 4k..4k+3 of both halves: a lane folds its 8
+// pixels in registers, a quad DPP reduction and one xor-32 swap give every
+// lane its block's tile box.
+__device__ __forceinline__ unsigned quad_min_pk16(unsigned v) {
     constexpr int ident = -1;
-    v = pk_min_u16(v, unsigned(__builtin_amdgcn_update_dpp(ident, int(v), 0xB1, 0xF, 0xF, false)));   // quad [1,0,3,2]
-    v = pk_min_u16(v, unsigned(__builtin_amdgcn_update_dpp(ident, int(v), 0x4E, 0xF, 0xF, false)));   // quad [2,3,0,1]
-    v = pk_min_u16(v, unsigned(__builtin_amdgcn_update_dpp(ident, int(v), 0x141, 0xF, 0xF, false)));  // row_half_mirror
-    v = pk_min_u16(v, unsigned(__builtin_amdgcn_update_dpp(ident, int(v), 0x140, 0xF, 0xF, false)));  // row_mirror
-    return v;
+    v = pk_min_u16(v, unsigned(__builtin_amdgcn_update_dpp(ident, int(v), 0xB1, 0xF, 0xF, false)));  // [1,0,3,2]
+    v = pk_min_u16(v, unsigned(__builtin_amdgcn_update_dpp(ident, int(v), 0x4E, 0xF, 0xF, false)));  // [2,3,0,1]
+    return pk_min_u16(v, unsigned(__shfl_xor(int(v), 32)));
 }
 
-template <typename Coords>
+template <typename Coords, bool kVec>
 __global__ __launch_bounds__(kWarpThreads) void bin_kernel(Coords co, const float *__restrict__ depth, ChunkArgs a,
                                                            int H, int W, int64_t HW, TileGeom g) {
     const Ws &ws = a.ws;
@@ -311,59 +344,59 @@ __global__ __launch_bounds__(kWarpThreads) void bin_kernel(Coords co, const floa
     const int sg = int(sgg - int64_t(bl) * g.nseg);
     const int sby = sg / g.nsegx, sgx = sg - sby * g.nsegx;
     const int64_t b = a.b0 + bl;
-    int tx[2][SBH], ty[2][SBH];
+    const int i0 = sgx * (SEGB * SBW) + (lane & 31) * 4;
+    const int jh = sby * SBH + (lane >> 5);
+    int tx[2][4], ty[2][4];
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int q = 0; q < 2; ++q) {
+        const int j = jh + 2 * q;
+        typename Coords::V x[4], y[4];
 #pragma unroll
-        for (int r = 0; r < SBH; ++r) {
-            const int i = sgx * (SEGB * SBW) + h * 64 + lane, j = sby * SBH + r;
-            tx[h][r] = ty[h][r] = -1;
-            if (i < W && j < H) {
-                typename Coords::V x, y;
-                co.load(b, int64_t(j) * W + i, x, y);
-                co.target(i, j, x, y, H, W, tx[h][r], ty[h][r]);
-            }
+        for (int e = 0; e < 4; ++e) tx[q][e] = ty[q][e] = -1;
+        if (i0 < W && j < H) {
+            co.template load4<kVec>(b, int64_t(j) * W + i0, x, y, W - i0);
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (i0 + e < W) co.target(i0 + e, j, x[e], y[e], H, W, tx[q][e], ty[q][e]);
         }
-    // per lane: packed (tile x, tile y) min and (0xFFFF - tile x, 0xFFFF - tile y) min
-    unsigned mn[2], mxi[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        unsigned m = 0xFFFFFFFFu, x = 0xFFFFFFFFu;
-#pragma unroll
-        for (int r = 0; r < SBH; ++r) {
-            if (tx[h][r] >= 0) {
-                const unsigned ttx = unsigned(tx[h][r] / TW), tty = unsigned(ty[h][r] / TH);
-                m = pk_min_u16(m, ttx | (tty << 16));
-                x = pk_min_u16(x, (0xFFFFu - ttx) | ((0xFFFFu - tty) << 16));
-            }
-        }
-        mn[h] = row16_min_pk16(m);
-        mxi[h] = row16_min_pk16(x);
     }
+    // per lane: packed (tile x, tile y) min and (0xFFFF - tile x, 0xFFFF - tile y) min
+    unsigned mn = 0xFFFFFFFFu, mxi = 0xFFFFFFFFu;
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            if (tx[q][e] >= 0) {
+                const unsigned ttx = unsigned(tx[q][e] / TW), tty = unsigned(ty[q][e] / TH);
+                mn = pk_min_u16(mn, ttx | (tty << 16));
+                mxi = pk_min_u16(mxi, (0xFFFFu - ttx) | ((0xFFFFu - tty) << 16));
+            }
+    mn = quad_min_pk16(mn);
+    mxi = quad_min_pk16(mxi);
     int s0x = 0x7FFFFFFF, s1x = -1, s0y = 0x7FFFFFFF, s1y = -1;
 #pragma unroll
     for (int k = 0; k < SEGB; ++k) {
         const int sbx = sgx * SEGB + k;
         if (sbx >= g.nsbx) break;  // wave-uniform
-        const int h = k / 4, src_lane = (k % 4) * 16;
-        const unsigned bmn = unsigned(__builtin_amdgcn_readlane(int(mn[h]), src_lane));
-        const unsigned bmx = unsigned(__builtin_amdgcn_readlane(int(mxi[h]), src_lane));
+        const unsigned bmn = unsigned(__builtin_amdgcn_readlane(int(mn), 4 * k));
+        const unsigned bmx = unsigned(__builtin_amdgcn_readlane(int(mxi), 4 * k));
         ushort4 rec = empty_box();
         if ((bmn & 0xFFFFu) != 0xFFFFu) {
             const int t0x = int(bmn & 0xFFFFu), t0y = int(bmn >> 16);
             const int t1x = int(0xFFFFu - (bmx & 0xFFFFu)), t1y = int(0xFFFFu - (bmx >> 16));
             if ((t1x - t0x + 1) * (t1y - t0y + 1) > MAX_TILES_PER_BLOCK) {
                 // non-smooth flow: this block's sources go through the key slab
-                const bool mine_lane = (lane >> 4) == (k % 4);
+                const bool mine_lane = ((lane & 31) >> 2) == k;
 #pragma unroll
-                for (int r = 0; r < SBH; ++r) {
-                    const bool ok = mine_lane && tx[h][r] >= 0;
-                    const int i = sgx * (SEGB * SBW) + h * 64 + lane, j = sby * SBH + r;
-                    const int64_t p = int64_t(j) * W + i;
-                    const unsigned long long key = ok ? make_key(depth[b * HW + p], unsigned(p)) : 0ull;
-                    wave_run_atomic_min(ws.keys + int64_t(bl) * HW, ok ? ty[h][r] * W + tx[h][r] : -1, key);
-                    if (ok) ws.flag[int64_t(bl) * g.ntiles + (ty[h][r] / TH) * g.tilesX + tx[h][r] / TW] = 0u;
-                }
+                for (int q = 0; q < 2; ++q)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const bool ok = mine_lane && tx[q][e] >= 0;
+                        const int64_t p = int64_t(jh + 2 * q) * W + i0 + e;
+                        const unsigned long long key = ok ? make_key(depth[b * HW + p], unsigned(p)) : 0ull;
+                        wave_run_atomic_min(ws.keys + int64_t(bl) * HW, ok ? ty[q][e] * W + tx[q][e] : -1, key);
+                        if (ok) ws.flag[int64_t(bl) * g.ntiles + (ty[q][e] / TH) * g.tilesX + tx[q][e] / TW] = 0u;
+                    }
             } else {
                 rec = make_ushort4((unsigned short)t0x, (unsigned short)t1x, (unsigned short)t0y,
                                    (unsigned short)t1y);
@@ -385,7 +418,7 @@ __global__ __launch_bounds__(kWarpThreads) void bin_kernel(Coords co, const floa
 // 8 XCDs (workgroups b and b+8 share one), so each XCD gets a contiguous run
 // of tiles -- neighbouring tiles share source blocks and box records in its
 // L2.  Placement only affects speed, never results.
-template <typename Coords, bool kStamp = false>
+template <typename Coords, bool kStamp = false, int kNTPub = 2>
 __global__ __launch_bounds__(kWarpThreads, 8) void splat_kernel(Coords co, const float *__restrict__ depth,
                                                                 float *__restrict__ valid, float *__restrict__ coll,
                                                                 ChunkArgs a, int H, int W, int64_t HW, TileGeom g,
@@ -537,9 +570,16 @@ __global__ __launch_bounds__(kWarpThreads, 8) void splat_kernel(Coords co, const
         const bool touched = key != KEY_UNTOUCHED;
         const bool nowin = key == KEY_NOWIN;
         const unsigned t = unsigned(ty) * unsigned(W) + unsigned(tx);
-        win[t] = (touched && !nowin) ? unsigned(key & 0xFFFFFFFFull) : WIN_NONE;
-        vb[t] = touched ? 1.f : 0.f;
-        cb[t] = nowin ? 1.f : 0.f;
+        const unsigned wv = (touched && !nowin) ? unsigned(key & 0xFFFFFFFFull) : WIN_NONE;
+        if constexpr (kNTPub >= 2) __builtin_nontemporal_store(wv, win + t);
+        else win[t] = wv;
+        if constexpr (kNTPub >= 1) {
+            __builtin_nontemporal_store(touched ? 1.f : 0.f, vb + t);
+            __builtin_nontemporal_store(nowin ? 1.f : 0.f, cb + t);
+        } else {
+            vb[t] = touched ? 1.f : 0.f;
+            cb[t] = nowin ? 1.f : 0.f;
+        }
     }
     if constexpr (kStamp) {
         __syncthreads();
@@ -548,23 +588,27 @@ __global__ __launch_bounds__(kWarpThreads, 8) void splat_kernel(Coords co, const
 }
 
 // ---- RESOLVE: one target per thread over 2-D target patches -- workgroup =
-// 64 columns x kRows rows (wave = one 64-pixel row segment), grid (x, y,
-// image) so no division is needed.  The gathers of vertically adjacent
-// targets, whose sources share cache lines under rotated / sheared flows, run
-// on one CU at the same time (64x16 measured 5 % faster than 256x1).  32-bit
-// offsets inside an image (C*H*W < 2^30 is checked on the host); the gathers
-// of up to kChan channels are in flight before the stores.
-template <int kChan, int kRows>
-__global__ __launch_bounds__(64 * kRows) void resolve2d_kernel(const float *__restrict__ obj,
-                                                               const unsigned int *__restrict__ winner,
-                                                               float *__restrict__ out, int C, int H, int W,
-                                                               int64_t HW, int64_t b0) {
-    const unsigned x = blockIdx.x * 64u + (threadIdx.x & 63u);
-    const unsigned y = blockIdx.y * unsigned(kRows) + (threadIdx.x >> 6);
+// 64*kWX columns x kRows rows (wave = one 64-pixel row segment), grid (x, y,
+// image) so no division is needed.  The gathers of neighbouring targets,
+// whose sources share cache lines under rotated / sheared flows, run on one
+// CU at the same time.  The output planes and the winner map are touched once,
+// so they go non-temporal (kNT / kNTW) and leave the caches to the gathered
+// source lines.  tools/probe_tile.py sweep at 64 x 768x1024, C=6: 128x8 nt
+// 462 us, 64x16 nt 474, 64x16 plain 487, 1024x1 plain 553.  32-bit offsets
+// inside an image (C*H*W < 2^30 is checked on the host); the gathers of up to
+// kChan channels are in flight before the stores.
+template <int kChan, int kRows, int kWX = 1, bool kNT = false, bool kNTW = false>
+__global__ __launch_bounds__(64 * kWX * kRows) void resolve2d_kernel(const float *__restrict__ obj,
+                                                                     const unsigned int *__restrict__ winner,
+                                                                     float *__restrict__ out, int C, int H, int W,
+                                                                     int64_t HW, int64_t b0) {
+    const unsigned wave = threadIdx.x >> 6;
+    const unsigned x = (blockIdx.x * unsigned(kWX) + wave % unsigned(kWX)) * 64u + (threadIdx.x & 63u);
+    const unsigned y = blockIdx.y * unsigned(kRows) + wave / unsigned(kWX);
     if (x >= unsigned(W) || y >= unsigned(H)) return;
     const int64_t bl = blockIdx.z, b = b0 + bl;
     const unsigned p = y * unsigned(W) + x;
-    const unsigned w = winner[bl * HW + p];
+    const unsigned w = kNTW ? __builtin_nontemporal_load(winner + bl * HW + p) : winner[bl * HW + p];
     const float *ob = obj + b * C * HW;
     float *oo = out + b * C * HW;
     const unsigned uHW = unsigned(HW);
@@ -576,7 +620,12 @@ __global__ __launch_bounds__(64 * kRows) void resolve2d_kernel(const float *__re
             o[cc] = (win && c0 + cc < C) ? ob[unsigned(c0 + cc) * uHW + w] : 0.f;
 #pragma unroll
         for (int cc = 0; cc < kChan; ++cc)
-            if (c0 + cc < C) oo[unsigned(c0 + cc) * uHW + p] = o[cc];
+            if (c0 + cc < C) {
+                if constexpr (kNT)
+                    __builtin_nontemporal_store(o[cc], oo + unsigned(c0 + cc) * uHW + p);
+                else
+                    oo[unsigned(c0 + cc) * uHW + p] = o[cc];
+            }
     }
 }
 
@@ -792,6 +841,7 @@ int run_f32(Coords co, const float *obj, const float *depth, float *out, float *
         if (e != hipSuccess) return int(e);
     }
     const Ws slab = carve(ws, G, HW, g);
+    const bool vec = W % 4 == 0 && co.vec_ok();  // 16-byte coordinate loads in BIN
     for (int64_t c = 0; c < nch; ++c) {
         const int64_t b0 = c * G;
         const int64_t nb = (B - b0) < G ? (B - b0) : G;
@@ -805,20 +855,25 @@ int run_f32(Coords co, const float *obj, const float *depth, float *out, float *
             if (c == nch - 1 && g_prof_stop) (void)hipEventRecord(g_prof_stop, st);
         } else {
             const ChunkArgs a{slab, b0, int(nb)};
-            hipLaunchKernelGGL((bin_kernel<Coords>), dim3(grid_for(nb * g.nseg, kWaves)), dim3(kWarpThreads), 0, st,
-                               co, depth, a, int(H), int(W), HW, g);
+            if (vec)
+                hipLaunchKernelGGL((bin_kernel<Coords, true>), dim3(grid_for(nb * g.nseg, kWaves)),
+                                   dim3(kWarpThreads), 0, st, co, depth, a, int(H), int(W), HW, g);
+            else
+                hipLaunchKernelGGL((bin_kernel<Coords, false>), dim3(grid_for(nb * g.nseg, kWaves)),
+                                   dim3(kWarpThreads), 0, st, co, depth, a, int(H), int(W), HW, g);
             const unsigned tiles = unsigned(nb * g.ntiles);
             hipLaunchKernelGGL((splat_kernel<Coords>), dim3((tiles + 7u) / 8u * 8u), dim3(kWarpThreads), 0, st,
                                co, depth, valid, coll, a, int(H), int(W), HW, g, nullptr);
-            const dim3 rgrid(unsigned((W + 63) / 64), unsigned((H + kResolveRows - 1) / kResolveRows),
-                             unsigned(nb));
+            const dim3 rgrid(unsigned((W + 64 * kResolveWX - 1) / (64 * kResolveWX)),
+                             unsigned((H + kResolveRows - 1) / kResolveRows), unsigned(nb));
+            const dim3 rblock(64 * kResolveWX * kResolveRows);
             if (c == 0 && g_prof_start) (void)hipEventRecord(g_prof_start, st);
             if (C <= 8)
-                hipLaunchKernelGGL((resolve2d_kernel<8, kResolveRows>), rgrid, dim3(64 * kResolveRows), 0, st, obj,
-                                   slab.winner, out, int(C), int(H), int(W), HW, b0);
+                hipLaunchKernelGGL((resolve2d_kernel<8, kResolveRows, kResolveWX, true, true>), rgrid, rblock, 0, st,
+                                   obj, slab.winner, out, int(C), int(H), int(W), HW, b0);
             else
-                hipLaunchKernelGGL((resolve2d_kernel<4, kResolveRows>), rgrid, dim3(64 * kResolveRows), 0, st, obj,
-                                   slab.winner, out, int(C), int(H), int(W), HW, b0);
+                hipLaunchKernelGGL((resolve2d_kernel<4, kResolveRows, kResolveWX, true, true>), rgrid, rblock, 0, st,
+                                   obj, slab.winner, out, int(C), int(H), int(W), HW, b0);
             if (c == nch - 1 && g_prof_stop) (void)hipEventRecord(g_prof_stop, st);
         }
     }

@@ -17,16 +17,46 @@ extern "C" int probe_launch(int which, const float *obj, const float *flow, cons
     const ChunkArgs a{carve(slab, nimg, HW, g), b0, nimg};
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (which == 0) {
-        hipLaunchKernelGGL((bin_kernel<FlowCoords<float>>), dim3(grid_for(int64_t(nimg) * g.nseg, kWaves)),
+        hipLaunchKernelGGL((bin_kernel<FlowCoords<float>, true>), dim3(grid_for(int64_t(nimg) * g.nseg, kWaves)),
                            dim3(kWarpThreads), 0, st, co, depth, a, int(H), int(W), HW, g);
-    } else if (which == 1) {
+    } else if (which == 1 || which == 3 || which == 4) {
+        // 1: product SPLAT (stamped, all publish stores non-temporal); 3 / 4: plain / nt valid+coll only
         const unsigned tiles = unsigned(nimg * g.ntiles);
-        hipLaunchKernelGGL((splat_kernel<FlowCoords<float>, true>), dim3((tiles + 7u) / 8u * 8u),
-                           dim3(kWarpThreads), 0, st, co, depth, valid, coll, a, int(H), int(W), HW, g, stamps);
+        const dim3 grid((tiles + 7u) / 8u * 8u);
+        if (which == 1)
+            hipLaunchKernelGGL((splat_kernel<FlowCoords<float>, true>), grid, dim3(kWarpThreads), 0, st, co, depth,
+                               valid, coll, a, int(H), int(W), HW, g, stamps);
+        else if (which == 3)
+            hipLaunchKernelGGL((splat_kernel<FlowCoords<float>, true, 0>), grid, dim3(kWarpThreads), 0, st, co, depth,
+                               valid, coll, a, int(H), int(W), HW, g, stamps);
+        else
+            hipLaunchKernelGGL((splat_kernel<FlowCoords<float>, true, 1>), grid, dim3(kWarpThreads), 0, st, co, depth,
+                               valid, coll, a, int(H), int(W), HW, g, stamps);
     } else {
-        hipLaunchKernelGGL((resolve2d_kernel<8, kResolveRows>),
-                           dim3(unsigned((W + 63) / 64), unsigned((H + kResolveRows - 1) / kResolveRows), unsigned(nimg)),
-                           dim3(64 * kResolveRows), 0, st, obj, a.ws.winner, out, int(C), int(H), int(W), HW, b0);
+        // which 2: product RESOLVE; 10+v: RESOLVE shape / store variants
+        const int v = which == 2 ? 0 : which - 10;
+#define RV(WX, R, NT, ...)                                                                                         \
+    hipLaunchKernelGGL((resolve2d_kernel<8, R, WX, NT __VA_OPT__(,) __VA_ARGS__>),                                                       \
+                       dim3(unsigned((W + 64 * WX - 1) / (64 * WX)), unsigned((H + R - 1) / R), unsigned(nimg)), \
+                       dim3(64 * WX * R), 0, st, obj, a.ws.winner, out, int(C), int(H), int(W), HW, b0)
+        switch (v) {
+        case 0: RV(kResolveWX, kResolveRows, true, true); break;
+        case 1: RV(1, 16, true, true); break;
+        case 2: RV(4, 4, false); break;
+        case 3: RV(1, 8, false); break;
+        case 4: RV(2, 4, false); break;
+        case 5: RV(1, 4, false); break;
+        case 6: RV(1, 16, true); break;
+        case 7: RV(2, 8, true); break;
+        case 8: RV(4, 4, true); break;
+        case 9: RV(8, 2, true); break;
+        case 10: RV(2, 4, true); break;
+        case 11: RV(2, 8, true, true); break;
+        case 12: RV(4, 4, true, true); break;
+        case 13: RV(16, 1, true); break;
+        default: return -1;
+        }
+#undef RV
     }
     return int(hipGetLastError());
 }

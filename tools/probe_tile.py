@@ -73,6 +73,46 @@ def main():
             print("per-step launch totals (us): " + "  ".join(f"{k}={v:.1f}" for k, v in zip(names, tot)) +
                   f"  sum={sum(tot):.1f}  ({B} images, chunks of {G})")
     ref = forward_warp_flow(obj, flow, depth)
+    if os.environ.get("SPLAT_SWEEP"):
+        # SPLAT publish-store variants (each run re-BINs first: SPLAT consumes the records)
+        for rep in range(2):
+            res = []
+            for which, nm in ((1, "nt all (product)"), (3, "plain"), (4, "nt valid/coll")):
+                ts = []
+                for _ in range(5):
+                    for c0 in range(0, B, G):
+                        lib.probe_launch(0, *base, c0, min(G, B - c0), stamps.data_ptr(), st)
+                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        e0.record()
+                        rc = lib.probe_launch(which, *base, c0, min(G, B - c0), stamps.data_ptr(), st)
+                        e1.record()
+                        torch.cuda.synchronize()
+                        assert rc == 0, rc
+                        ts.append(e0.elapsed_time(e1) * 1e3)
+                res.append(f"{nm}={np.median(ts):.1f}")
+            if rep == 1:
+                print(f"SPLAT variants, chunks of {G}, median (us): " + "  ".join(res))
+    if os.environ.get("RESOLVE_SWEEP"):
+        # RESOLVE variants over the winner map of the last chunk (G images)
+        names_v = ["product", "1x16nt+ntw", "4x4", "1x8", "2x4", "1x4", "1x16nt", "2x8nt", "4x4nt", "8x2nt", "2x4nt",
+                   "2x8nt+ntw", "4x4nt+ntw", "16x1nt"]
+        c0 = B - G
+        for rep in range(2):
+            res = []
+            for v in range(len(names_v)):
+                ts = []
+                for _ in range(5):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    rc = lib.probe_launch(10 + v, *base, c0, G, stamps.data_ptr(), st)
+                    e1.record()
+                    torch.cuda.synchronize()
+                    assert rc == 0, rc
+                    ts.append(e0.elapsed_time(e1) * 1e3)
+                ok_v = torch.equal(out[c0:], ref[0][c0:])
+                res.append(f"{names_v[v]}={np.median(ts):.1f}{'' if ok_v else '(BAD)'}")
+            if rep == 1:
+                print(f"RESOLVE variants, {G} images, median of 5 (us): " + "  ".join(res))
     ok = all(torch.equal(x, y) for x, y in zip((out, valid, coll), ref))
     print("probe result == product result:", ok)
 
