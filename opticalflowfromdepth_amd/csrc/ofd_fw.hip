@@ -69,7 +69,7 @@ constexpr int TW = 128, TH = 32;          // target tile (LDS z-buffer 32 KiB)
 constexpr int SBW = 16, SBH = 4;          // source block = one wave (64 px)
 constexpr int SEGB = 8;                   // source blocks per segment (128 x 4 px)
 constexpr int MAX_TILES_PER_BLOCK = 12;   // wider boxes go through the global path
-constexpr int kSplatU = 12;               // source blocks in flight per wave (SPLAT)
+constexpr int kSplatU = 2;                // 4-block slots in flight per wave (SPLAT, f32 coords; 3 spills)
 
 // Default chunk: 64M source pixels (85 images of 768x1024, a ~830 MB slab).
 // Every kernel of a chunk then has a grid many times the resident slots
@@ -416,9 +416,28 @@ __global__ __launch_bounds__(kWarpThreads) void bin_kernel(Coords co, const floa
 
 // ---- SPLAT.  Workgroup id -> XCD-aware tile: dispatch is round-robin over the
 // 8 XCDs (workgroups b and b+8 share one), so each XCD gets a contiguous run
-// of tiles -- neighbouring tiles share source blocks and box records in its
-// L2.  Placement only affects speed, never results.
-template <typename Coords, bool kStamp = false, int kNTPub = 2>
+// of a band-major tile order -- tile-row band k of every image in turn -- so
+// neighbouring tiles share source blocks and box records in one L2, and every
+// XCD sees every image (whole images per XCD left the XCDs holding the
+// heavier ego-motion images running ~60 us after the rest had drained).
+// Placement only affects speed, never results.
+__device__ __forceinline__ void band_major_tile(unsigned lin, int nimg, const TileGeom &g, int &bl, int &tile) {
+    unsigned start = 0;
+    for (int k = 0; k < 8; ++k) {
+        const int r0 = k * g.tilesY / 8, r1 = (k + 1) * g.tilesY / 8;
+        const unsigned per_img = unsigned(r1 - r0) * unsigned(g.tilesX);
+        const unsigned cnt = per_img * unsigned(nimg);
+        if (lin < start + cnt || k == 7) {
+            const unsigned idx = lin - start;
+            bl = int(idx / per_img);
+            tile = r0 * g.tilesX + int(idx - unsigned(bl) * per_img);
+            return;
+        }
+        start += cnt;
+    }
+}
+
+template <typename Coords, bool kVec, bool kStamp = false, int kNTPub = 1, int kUF = kSplatU, int kMap = 0>
 __global__ __launch_bounds__(kWarpThreads, 8) void splat_kernel(Coords co, const float *__restrict__ depth,
                                                                 float *__restrict__ valid, float *__restrict__ coll,
                                                                 ChunkArgs a, int H, int W, int64_t HW, TileGeom g,
@@ -432,8 +451,22 @@ __global__ __launch_bounds__(kWarpThreads, 8) void splat_kernel(Coords co, const
     if constexpr (kStamp) { if (threadIdx.x == 0) ph[0] = wall_clock64(); }
 
     const Ws &ws = a.ws;
-    const int bl = int(lin / unsigned(g.ntiles));
-    const int tile = int(lin - unsigned(bl) * unsigned(g.ntiles));
+    int bl, tile;
+    if constexpr (kMap == 0) {
+        band_major_tile(lin, a.nimg, g, bl, tile);
+    } else if constexpr (kMap == 1) {  // whole images, image k, k+8, ... on XCD k
+        const unsigned s0 = lin / unsigned(g.ntiles);
+        tile = int(lin - s0 * unsigned(g.ntiles));
+        const unsigned nq = unsigned(a.nimg) / 8u, nr = unsigned(a.nimg) % 8u;
+        // s0-th image of the order sorted by (image % 8, image / 8)
+        unsigned k = 0, before = 0;
+        while (before + nq + (k < nr ? 1u : 0u) <= s0) { before += nq + (k < nr ? 1u : 0u); ++k; }
+        bl = int((s0 - before) * 8u + k);
+    } else {  // whole images, contiguous
+        bl = int(lin / unsigned(g.ntiles));
+        tile = int(lin - unsigned(bl) * unsigned(g.ntiles));
+    }
+    const unsigned fid = unsigned(bl) * unsigned(g.ntiles) + unsigned(tile);  // flag slot
     const int tyi = tile / g.tilesX, txi = tile - tyi * g.tilesX;
     const int x0 = txi * TW, y0 = tyi * TH;
     const int64_t b = a.b0 + bl;
@@ -442,8 +475,8 @@ __global__ __launch_bounds__(kWarpThreads, 8) void splat_kernel(Coords co, const
     const ushort4 *blkrec = ws.blkrec + int64_t(bl) * g.nsb;
 
     if (threadIdx.x == 0) {
-        L.flag = ws.flag[lin];
-        ws.flag[lin] = 0xFFFFFFFFu;  // restore the workspace invariant for the next call
+        L.flag = ws.flag[fid];
+        ws.flag[fid] = 0xFFFFFFFFu;  // restore the workspace invariant for the next call
         L.nseg = 0;
         L.nblk = 0;
     }
@@ -496,42 +529,48 @@ __global__ __launch_bounds__(kWarpThreads, 8) void splat_kernel(Coords co, const
             }
         }
         __syncthreads();
-        // ---- 3. splat the selected blocks into the LDS z-buffer.  One wave per
-        // source block (block id wave-uniform, pixel = lane), kSplatU blocks in
-        // flight per wave: every lane holds 3*kSplatU loads at once.
+        // ---- 3. splat the selected blocks into the LDS z-buffer.  A slot is 4
+        // blocks: lane = (block lane/16, row (lane/4)%4, pixels 4*(lane%4)..+3),
+        // one 16-byte load per plane (kVec); kU slots in flight per wave.
+        using V = typename Coords::V;
+        constexpr int kU = sizeof(V) == 4 ? kUF : 1;  // 64-VGPR budget
         const int nb = int(L.nblk);
-        for (int e0 = wave; e0 < nb; e0 += kWaves * kSplatU) {
-            typename Coords::V cx[kSplatU], cy[kSplatU];
-            float d[kSplatU];
+        const int sub = lane >> 4, rr = (lane >> 2) & 3, c4 = (lane & 3) * 4;
+        for (int e0 = wave * 4; e0 < nb; e0 += kWaves * 4 * kU) {
+            V cx[kU][4], cy[kU][4];
+            float d[kU][4];
+            int ii[kU], jj[kU];
 #pragma unroll
-            for (int u = 0; u < kSplatU; ++u) {
-                const int e = e0 + u * kWaves;
-                cx[u] = cy[u] = typename Coords::V(0);
-                d[u] = 0.f;
+            for (int u = 0; u < kU; ++u) {
+                const int e = e0 + sub + u * kWaves * 4;
+                ii[u] = W;
+                jj[u] = 0;
                 if (e < nb) {
-                    const int sb = __builtin_amdgcn_readfirstlane(int(L.blk[e]));
+                    const int sb = int(L.blk[e]);
                     const int sby = sb / g.nsbx, sbx = sb - sby * g.nsbx;
-                    const int i = sbx * SBW + (lane % SBW), j = sby * SBH + (lane / SBW);
+                    const int i = sbx * SBW + c4, j = sby * SBH + rr;
                     if (i < W && j < H) {
+                        ii[u] = i;
+                        jj[u] = j;
                         const int64_t p = int64_t(j) * W + i;
-                        co.load(b, p, cx[u], cy[u]);
-                        d[u] = depth[b * HW + p];
+                        co.template load4<kVec>(b, p, cx[u], cy[u], W - i);
+                        load4<kVec>(depth + b * HW + p, d[u], W - i);
                     }
                 }
             }
 #pragma unroll
-            for (int u = 0; u < kSplatU; ++u) {
-                const int e = e0 + u * kWaves;
-                if (e >= nb) break;  // wave-uniform
-                const int sb = __builtin_amdgcn_readfirstlane(int(L.blk[e]));
-                const int sby = sb / g.nsbx, sbx = sb - sby * g.nsbx;
-                const int i = sbx * SBW + (lane % SBW), j = sby * SBH + (lane / SBW);
-                if (i >= W || j >= H) continue;
-                int tx, ty;
-                co.target(i, j, cx[u], cy[u], H, W, tx, ty);
-                const int lx = tx - x0, ly = ty - y0;
-                if (tx >= 0 && unsigned(lx) < unsigned(TW) && unsigned(ly) < unsigned(TH))
-                    atomicMin(&L.zk[ly * TW + lx], make_key(d[u], unsigned(j * W + i)));
+            for (int u = 0; u < kU; ++u) {
+                if (ii[u] >= W) continue;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int i = ii[u] + q, j = jj[u];
+                    if (i >= W) break;
+                    int tx, ty;
+                    co.target(i, j, cx[u][q], cy[u][q], H, W, tx, ty);
+                    const int lx = tx - x0, ly = ty - y0;
+                    if (tx >= 0 && unsigned(lx) < unsigned(TW) && unsigned(ly) < unsigned(TH))
+                        atomicMin(&L.zk[ly * TW + lx], make_key(d[u][q], unsigned(j * W + i)));
+                }
             }
         }
         __syncthreads();
@@ -841,7 +880,8 @@ int run_f32(Coords co, const float *obj, const float *depth, float *out, float *
         if (e != hipSuccess) return int(e);
     }
     const Ws slab = carve(ws, G, HW, g);
-    const bool vec = W % 4 == 0 && co.vec_ok();  // 16-byte coordinate loads in BIN
+    // 16-byte coordinate / depth loads in BIN and SPLAT
+    const bool vec = W % 4 == 0 && co.vec_ok() && uintptr_t(depth) % 16 == 0;
     for (int64_t c = 0; c < nch; ++c) {
         const int64_t b0 = c * G;
         const int64_t nb = (B - b0) < G ? (B - b0) : G;
@@ -862,8 +902,12 @@ int run_f32(Coords co, const float *obj, const float *depth, float *out, float *
                 hipLaunchKernelGGL((bin_kernel<Coords, false>), dim3(grid_for(nb * g.nseg, kWaves)),
                                    dim3(kWarpThreads), 0, st, co, depth, a, int(H), int(W), HW, g);
             const unsigned tiles = unsigned(nb * g.ntiles);
-            hipLaunchKernelGGL((splat_kernel<Coords>), dim3((tiles + 7u) / 8u * 8u), dim3(kWarpThreads), 0, st,
-                               co, depth, valid, coll, a, int(H), int(W), HW, g, nullptr);
+            if (vec)
+                hipLaunchKernelGGL((splat_kernel<Coords, true>), dim3((tiles + 7u) / 8u * 8u), dim3(kWarpThreads), 0,
+                                   st, co, depth, valid, coll, a, int(H), int(W), HW, g, nullptr);
+            else
+                hipLaunchKernelGGL((splat_kernel<Coords, false>), dim3((tiles + 7u) / 8u * 8u), dim3(kWarpThreads),
+                                   0, st, co, depth, valid, coll, a, int(H), int(W), HW, g, nullptr);
             const dim3 rgrid(unsigned((W + 64 * kResolveWX - 1) / (64 * kResolveWX)),
                              unsigned((H + kResolveRows - 1) / kResolveRows), unsigned(nb));
             const dim3 rblock(64 * kResolveWX * kResolveRows);

@@ -19,18 +19,38 @@ extern "C" int probe_launch(int which, const float *obj, const float *flow, cons
     if (which == 0) {
         hipLaunchKernelGGL((bin_kernel<FlowCoords<float>, true>), dim3(grid_for(int64_t(nimg) * g.nseg, kWaves)),
                            dim3(kWarpThreads), 0, st, co, depth, a, int(H), int(W), HW, g);
+    } else if (which == 7 || which == 8) {
+        // SPLAT tile orders: 7 = whole images strided over XCDs, 8 = whole images contiguous
+        const unsigned tiles = unsigned(nimg * g.ntiles);
+        const dim3 grid((tiles + 7u) / 8u * 8u);
+        if (which == 7)
+            hipLaunchKernelGGL((splat_kernel<FlowCoords<float>, true, true, 2, kSplatU, 1>), grid, dim3(kWarpThreads), 0,
+                               st, co, depth, valid, coll, a, int(H), int(W), HW, g, stamps);
+        else
+            hipLaunchKernelGGL((splat_kernel<FlowCoords<float>, true, true, 2, kSplatU, 2>), grid, dim3(kWarpThreads), 0,
+                               st, co, depth, valid, coll, a, int(H), int(W), HW, g, stamps);
+    } else if (which == 5 || which == 6) {
+        // SPLAT with 3 / 4 slots of 4 blocks in flight per wave
+        const unsigned tiles = unsigned(nimg * g.ntiles);
+        const dim3 grid((tiles + 7u) / 8u * 8u);
+        if (which == 5)
+            hipLaunchKernelGGL((splat_kernel<FlowCoords<float>, true, true, 2, 3>), grid, dim3(kWarpThreads), 0, st, co,
+                               depth, valid, coll, a, int(H), int(W), HW, g, stamps);
+        else
+            hipLaunchKernelGGL((splat_kernel<FlowCoords<float>, true, true, 2, 4>), grid, dim3(kWarpThreads), 0, st, co,
+                               depth, valid, coll, a, int(H), int(W), HW, g, stamps);
     } else if (which == 1 || which == 3 || which == 4) {
-        // 1: product SPLAT (stamped, all publish stores non-temporal); 3 / 4: plain / nt valid+coll only
+        // 1: product SPLAT (stamped; valid / collision non-temporal); 3 / 4: all plain / all non-temporal
         const unsigned tiles = unsigned(nimg * g.ntiles);
         const dim3 grid((tiles + 7u) / 8u * 8u);
         if (which == 1)
-            hipLaunchKernelGGL((splat_kernel<FlowCoords<float>, true>), grid, dim3(kWarpThreads), 0, st, co, depth,
+            hipLaunchKernelGGL((splat_kernel<FlowCoords<float>, true, true>), grid, dim3(kWarpThreads), 0, st, co, depth,
                                valid, coll, a, int(H), int(W), HW, g, stamps);
         else if (which == 3)
-            hipLaunchKernelGGL((splat_kernel<FlowCoords<float>, true, 0>), grid, dim3(kWarpThreads), 0, st, co, depth,
+            hipLaunchKernelGGL((splat_kernel<FlowCoords<float>, true, true, 0>), grid, dim3(kWarpThreads), 0, st, co, depth,
                                valid, coll, a, int(H), int(W), HW, g, stamps);
         else
-            hipLaunchKernelGGL((splat_kernel<FlowCoords<float>, true, 1>), grid, dim3(kWarpThreads), 0, st, co, depth,
+            hipLaunchKernelGGL((splat_kernel<FlowCoords<float>, true, true, 2>), grid, dim3(kWarpThreads), 0, st, co, depth,
                                valid, coll, a, int(H), int(W), HW, g, stamps);
     } else {
         // which 2: product RESOLVE; 10+v: RESOLVE shape / store variants

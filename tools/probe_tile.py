@@ -69,29 +69,40 @@ def main():
                     print(f"chunk {c0:3d}: splat wg phase medians " +
                           "  ".join(f"{k}={np.median(v):5.1f}" for k, v in zip(pn, ph)) +
                           f"  p99 total={np.percentile(ph[4], 99):.1f}  nseg median={np.median(s[:, 7]):.0f}")
+                    span = (s[:, 1].max() - s[:, 0].min()) / 100.0
+                    print(f"           splat span {span:.1f} us, mean resident workgroups "
+                          f"{ph[4].sum() / span:.0f}, first-wave start spread "
+                          f"{(np.sort(s[:, 0])[1023] - s[:, 0].min()) / 100.0:.1f} us")
+                    t0s, t1s = s[:, 0] - s[:, 0].min(), s[:, 1] - s[:, 0].min()
+                    pts = np.linspace(0, t1s.max(), 13)[:-1]
+                    act = [int(((t0s <= t) & (t1s > t)).sum()) for t in pts]
+                    print("           resident workgroups at 12 points of the span: " + " ".join(map(str, act)))
         if rep == 1:
             print("per-step launch totals (us): " + "  ".join(f"{k}={v:.1f}" for k, v in zip(names, tot)) +
                   f"  sum={sum(tot):.1f}  ({B} images, chunks of {G})")
     ref = forward_warp_flow(obj, flow, depth)
     if os.environ.get("SPLAT_SWEEP"):
-        # SPLAT publish-store variants (each run re-BINs first: SPLAT consumes the records)
-        for rep in range(2):
-            res = []
-            for which, nm in ((1, "nt all (product)"), (3, "plain"), (4, "nt valid/coll")):
-                ts = []
-                for _ in range(5):
-                    for c0 in range(0, B, G):
-                        lib.probe_launch(0, *base, c0, min(G, B - c0), stamps.data_ptr(), st)
-                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                        e0.record()
-                        rc = lib.probe_launch(which, *base, c0, min(G, B - c0), stamps.data_ptr(), st)
-                        e1.record()
-                        torch.cuda.synchronize()
-                        assert rc == 0, rc
-                        ts.append(e0.elapsed_time(e1) * 1e3)
-                res.append(f"{nm}={np.median(ts):.1f}")
-            if rep == 1:
-                print(f"SPLAT variants, chunks of {G}, median (us): " + "  ".join(res))
+        # SPLAT variants, interleaved round-robin over 15 rounds (each run
+        # re-BINs first: SPLAT consumes the records); median per variant
+        variants = ((1, "product"), (3, "plain stores"), (4, "nt all"), (5, "3 slots"),
+                    (7, "images strided over XCDs"), (8, "images contiguous"))
+        ts = {nm: [] for _, nm in variants}
+        for rnd in range(16):
+            for which, nm in variants:
+                tot = 0.0
+                for c0 in range(0, B, G):
+                    lib.probe_launch(0, *base, c0, min(G, B - c0), stamps.data_ptr(), st)
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    rc = lib.probe_launch(which, *base, c0, min(G, B - c0), stamps.data_ptr(), st)
+                    e1.record()
+                    torch.cuda.synchronize()
+                    assert rc == 0, rc
+                    tot += e0.elapsed_time(e1) * 1e3
+                if rnd > 0:
+                    ts[nm].append(tot)
+        print(f"SPLAT variants, chunks of {G}, median of 15 interleaved (us): " +
+              "  ".join(f"{nm}={np.median(v):.1f}" for nm, v in ts.items()))
     if os.environ.get("RESOLVE_SWEEP"):
         # RESOLVE variants over the winner map of the last chunk (G images)
         names_v = ["product", "1x16nt+ntw", "4x4", "1x8", "2x4", "1x4", "1x16nt", "2x8nt", "4x4nt", "8x2nt", "2x4nt",
