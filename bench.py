@@ -163,7 +163,7 @@ def main():
     # dominant kernel: RESOLVE (tile engine) gathers obj and writes the C output
     # planes; the atomic engine's resolve pass also writes valid / collision
     kern_bpp = (2 * C) * 4 if args.engine == "tile" else (2 * C + 2) * 4
-    kern_name = "resolve_kernel" if args.engine == "tile" else "resolve_atomic_kernel"
+    kern_name = "resolve2d_kernel" if args.engine == "tile" else "resolve_atomic_kernel"
     kern_gbs = px_step_rank * kern_bpp / (resolve_ms / 1e3) / 1e9
 
     traffic = traffic_step = None

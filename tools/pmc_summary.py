@@ -35,7 +35,7 @@ def main():
     f = per_dispatch(fd)
     w = per_dispatch(wd)
     names = [x[0] for x in f]
-    per_call = 3 if "resolve_kernel" in names else 2
+    per_call = 3 if "bin_kernel" in names else 2  # tile engine: BIN, SPLAT, RESOLVE
     f, w = f[-per_call:], w[-per_call:]
     rep = {"config": [B, C, H, W], "kernels": []}
     tot_r = tot_w = 0.0
