@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline wall budget")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
     ap.add_argument("--check", action="store_true", help="verify one image against the oracle")
-    ap.add_argument("--engine", choices=["tile", "atomic"], default="tile")
+    ap.add_argument("--engine", choices=["tile", "split", "atomic"], default="tile")
     return ap.parse_args()
 
 
@@ -110,7 +110,7 @@ def main():
                                              camera=(s_all[a:b], T_all[a:b]))
     C = obj.shape[1]
     out = (torch.empty_like(obj), torch.empty_like(depth), torch.empty_like(depth))
-    _native.lib().ofd_fw_set_engine(0 if args.engine == "tile" else 1)
+    _native.lib().ofd_fw_set_engine({"tile": 0, "atomic": 1, "split": 2}[args.engine])
     torch.cuda.synchronize()
 
     for _ in range(args.warmup):
@@ -135,7 +135,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        # events around the dominant kernel (RESOLVE), recorded by the library
+        # events around the dominant kernel, recorded by the library
         # on the launch stream (include/ofd_fw.h: ofd_fw_set_profile_events)
         lib.ofd_fw_set_profile_events(rstarts[k].cuda_event, rends[k].cuda_event)
         starts[k].record(stream)
@@ -160,19 +160,24 @@ def main():
     bytes_per_px = (2 * C + 5) * 4  # algorithmic: obj C + flow 2 + depth in; out C + valid + coll
     value = n_total * H * W * args.steps / wall / 1e6
     achieved_gbs = px_step_rank * bytes_per_px / (dev_ms / 1e3) / 1e9
-    # dominant kernel: RESOLVE (tile engine) gathers obj and writes the C output
-    # planes; the atomic engine's resolve pass also writes valid / collision
-    kern_bpp = (2 * C) * 4 if args.engine == "tile" else (2 * C + 2) * 4
-    kern_name = "resolve2d_kernel" if args.engine == "tile" else "resolve_atomic_kernel"
+    # dominant kernel and its algorithmic bytes per source pixel:
+    #   tile  : SPLAT reads flow, depth and obj, writes output, valid and
+    #           collision -- every algorithmic byte of the op, (2C+5)*4
+    #           (BIN's flow read is the one re-read)
+    #   split : RESOLVE gathers obj and writes the C output planes, 2C*4
+    #   atomic: the resolve pass also writes valid / collision, (2C+2)*4
+    kern_bpp, kern_name = {"tile": ((2 * C + 5) * 4, "splat_kernel"),
+                           "split": (2 * C * 4, "resolve2d_kernel"),
+                           "atomic": ((2 * C + 2) * 4, "resolve_atomic_kernel")}[args.engine]
     kern_gbs = px_step_rank * kern_bpp / (resolve_ms / 1e3) / 1e9
 
     traffic = traffic_step = None
     traffic_note = None
     pmc_file = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc_file) and args.engine == "tile":
+    if os.path.exists(pmc_file) and args.engine != "atomic":
         try:
             pm = json.load(open(pmc_file))
-            if pm.get("config") == [B, C, H, W]:
+            if pm.get("config") == [B, C, H, W] and pm.get("engine", "split") == args.engine:
                 traffic_step = pm.get("hbm_bytes_per_step")
                 for kk in pm.get("kernels", []):
                     if kk["kernel"] == kern_name:

@@ -59,19 +59,22 @@ enum {
 /* ABI version of the loaded library (OFD_FW_ABI_VERSION at build time). */
 int ofd_fw_abi_version(void);
 
-/* Engines (see csrc/ofd_fw.hip): TILE = LDS z-buffer per target tile (default);
- * ATOMIC = one global 64-bit atomic min per source.  Results are identical.
+/* Engines (see csrc/ofd_fw.hip): TILE = LDS z-buffer per target tile whose
+ * workgroup also gathers the output (default); TILE_SPLIT = the same z-buffer
+ * publishing a winner map, then a separate RESOLVE gather pass; ATOMIC = one
+ * global 64-bit atomic min per source.  Results are identical.
  * Selects the engine for subsequent calls in this process (also settable with
- * OFD_FW_MODE=atomic); an unknown value only queries.  Returns the previous
- * engine.  Not thread-safe against concurrent calls. */
+ * OFD_FW_MODE=atomic|split); an unknown value only queries.  Returns the
+ * previous engine.  Not thread-safe against concurrent calls. */
 #define OFD_FW_ENGINE_TILE 0
 #define OFD_FW_ENGINE_ATOMIC 1
+#define OFD_FW_ENGINE_TILE_SPLIT 2
 int ofd_fw_set_engine(int engine);
 
 /* Benchmark hook: when non-NULL, the given hipEvent_t's are recorded on the
- * launch stream right before the first and right after the last RESOLVE
- * launch of each subsequent f32 call (RESOLVE is the dominant kernel; the
- * ATOMIC engine's resolve pass likewise).  Pass NULLs to disable.  Process-
+ * launch stream right before the first and right after the last launch of
+ * each subsequent f32 call's dominant kernel: SPLAT (TILE engine), RESOLVE
+ * (TILE_SPLIT), the resolve pass (ATOMIC).  Pass NULLs to disable.  Process-
  * wide, not thread-safe; for timing only. */
 int ofd_fw_set_profile_events(void *start_event, void *stop_event);
 

@@ -70,6 +70,7 @@ constexpr int SBW = 16, SBH = 4;          // source block = one wave (64 px)
 constexpr int SEGB = 8;                   // source blocks per segment (128 x 4 px)
 constexpr int MAX_TILES_PER_BLOCK = 12;   // wider boxes go through the global path
 constexpr int kSplatU = 2;                // 4-block slots in flight per wave (SPLAT, f32 coords; 3 spills)
+constexpr int kBinSPW = 1;                // segments per BIN wave (2 / 4: 125 / 192 us vs 96 at 64 images)
 
 // Default chunk: 64M source pixels (85 images of 768x1024, a ~830 MB slab).
 // Every kernel of a chunk then has a grid many times the resident slots
@@ -333,13 +334,12 @@ __device__ __forceinline__ unsigned quad_min_pk16(unsigned v) {
     return pk_min_u16(v, unsigned(__shfl_xor(int(v), 32)));
 }
 
-template <typename Coords, bool kVec>
-__global__ __launch_bounds__(kWarpThreads) void bin_kernel(Coords co, const float *__restrict__ depth, ChunkArgs a,
-                                                           int H, int W, int64_t HW, TileGeom g) {
+template <typename Coords>
+__device__ __forceinline__ void bin_segment(const Coords &co, const float *__restrict__ depth, const ChunkArgs &a,
+                                            int H, int W, int64_t HW, const TileGeom &g, int64_t sgg,
+                                            const typename Coords::V (&x)[2][4], const typename Coords::V (&y)[2][4]) {
     const Ws &ws = a.ws;
     const int lane = lane_id();
-    const int64_t sgg = int64_t(blockIdx.x) * kWaves + (threadIdx.x >> 6);
-    if (sgg >= int64_t(a.nimg) * g.nseg) return;  // wave-uniform
     const int bl = int(sgg / g.nseg);
     const int sg = int(sgg - int64_t(bl) * g.nseg);
     const int sby = sg / g.nsegx, sgx = sg - sby * g.nsegx;
@@ -350,14 +350,10 @@ __global__ __launch_bounds__(kWarpThreads) void bin_kernel(Coords co, const floa
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
         const int j = jh + 2 * q;
-        typename Coords::V x[4], y[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) tx[q][e] = ty[q][e] = -1;
-        if (i0 < W && j < H) {
-            co.template load4<kVec>(b, int64_t(j) * W + i0, x, y, W - i0);
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-                if (i0 + e < W) co.target(i0 + e, j, x[e], y[e], H, W, tx[q][e], ty[q][e]);
+        for (int e = 0; e < 4; ++e) {
+            tx[q][e] = ty[q][e] = -1;
+            if (i0 + e < W && j < H) co.target(i0 + e, j, x[q][e], y[q][e], H, W, tx[q][e], ty[q][e]);
         }
     }
     // per lane: packed (tile x, tile y) min and (0xFFFF - tile x, 0xFFFF - tile y) min
@@ -374,6 +370,7 @@ __global__ __launch_bounds__(kWarpThreads) void bin_kernel(Coords co, const floa
     mn = quad_min_pk16(mn);
     mxi = quad_min_pk16(mxi);
     int s0x = 0x7FFFFFFF, s1x = -1, s0y = 0x7FFFFFFF, s1y = -1;
+    unsigned wide = 0;  // wave-uniform: blocks whose sources go through the key slab
 #pragma unroll
     for (int k = 0; k < SEGB; ++k) {
         const int sbx = sgx * SEGB + k;
@@ -385,18 +382,7 @@ __global__ __launch_bounds__(kWarpThreads) void bin_kernel(Coords co, const floa
             const int t0x = int(bmn & 0xFFFFu), t0y = int(bmn >> 16);
             const int t1x = int(0xFFFFu - (bmx & 0xFFFFu)), t1y = int(0xFFFFu - (bmx >> 16));
             if ((t1x - t0x + 1) * (t1y - t0y + 1) > MAX_TILES_PER_BLOCK) {
-                // non-smooth flow: this block's sources go through the key slab
-                const bool mine_lane = ((lane & 31) >> 2) == k;
-#pragma unroll
-                for (int q = 0; q < 2; ++q)
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const bool ok = mine_lane && tx[q][e] >= 0;
-                        const int64_t p = int64_t(jh + 2 * q) * W + i0 + e;
-                        const unsigned long long key = ok ? make_key(depth[b * HW + p], unsigned(p)) : 0ull;
-                        wave_run_atomic_min(ws.keys + int64_t(bl) * HW, ok ? ty[q][e] * W + tx[q][e] : -1, key);
-                        if (ok) ws.flag[int64_t(bl) * g.ntiles + (ty[q][e] / TH) * g.tilesX + tx[q][e] / TW] = 0u;
-                    }
+                wide |= 1u << k;  // non-smooth flow: spilled below
             } else {
                 rec = make_ushort4((unsigned short)t0x, (unsigned short)t1x, (unsigned short)t0y,
                                    (unsigned short)t1y);
@@ -412,6 +398,53 @@ __global__ __launch_bounds__(kWarpThreads) void bin_kernel(Coords co, const floa
         ws.segrec[sgg] = s1x < 0 ? empty_box()
                                  : make_ushort4((unsigned short)s0x, (unsigned short)s1x, (unsigned short)s0y,
                                                 (unsigned short)s1y);
+    if (wide == 0u) return;
+    // non-smooth flow (rare): the wide blocks' sources go to the key slab by
+    // global atomic min and flag their target tiles for SPLAT's merge
+#pragma unroll 1
+    for (int k = 0; k < SEGB; ++k) {
+        if (!((wide >> k) & 1u)) continue;
+        const bool mine_lane = ((lane & 31) >> 2) == k;
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const bool ok = mine_lane && tx[q][e] >= 0;
+                const int64_t p = int64_t(jh + 2 * q) * W + i0 + e;
+                const unsigned long long key = ok ? make_key(depth[b * HW + p], unsigned(p)) : 0ull;
+                wave_run_atomic_min(ws.keys + int64_t(bl) * HW, ok ? ty[q][e] * W + tx[q][e] : -1, key);
+                if (ok) ws.flag[int64_t(bl) * g.ntiles + (ty[q][e] / TH) * g.tilesX + tx[q][e] / TW] = 0u;
+            }
+    }
+}
+
+// kSPW segments per wave (consecutive in the image's segment order): every
+// segment's coordinate loads are issued before the first one is folded.
+template <typename Coords, bool kVec, int kSPW = 1>
+__global__ __launch_bounds__(kWarpThreads) void bin_kernel(Coords co, const float *__restrict__ depth, ChunkArgs a,
+                                                           int H, int W, int64_t HW, TileGeom g) {
+    using V = typename Coords::V;
+    const int lane = lane_id();
+    const int64_t sg0 = (int64_t(blockIdx.x) * kWaves + (threadIdx.x >> 6)) * kSPW;
+    const int64_t nsg = int64_t(a.nimg) * g.nseg;
+    V x[kSPW][2][4], y[kSPW][2][4];
+#pragma unroll
+    for (int s = 0; s < kSPW; ++s) {
+        const int64_t sgg = sg0 + s < nsg ? sg0 + s : nsg - 1;  // a clamped duplicate is loaded, not binned
+        const int bl = int(sgg / g.nseg);
+        const int sg = int(sgg - int64_t(bl) * g.nseg);
+        const int sby = sg / g.nsegx, sgx = sg - sby * g.nsegx;
+        const int i0 = sgx * (SEGB * SBW) + (lane & 31) * 4;
+        const int jh = sby * SBH + (lane >> 5);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int j = jh + 2 * q;
+            if (i0 < W && j < H) co.template load4<kVec>(a.b0 + bl, int64_t(j) * W + i0, x[s][q], y[s][q], W - i0);
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < kSPW; ++s)
+        if (sg0 + s < nsg) bin_segment(co, depth, a, H, W, HW, g, sg0 + s, x[s], y[s]);  // wave-uniform
 }
 
 // ---- SPLAT.  Workgroup id -> XCD-aware tile: dispatch is round-robin over the
@@ -437,11 +470,21 @@ __device__ __forceinline__ void band_major_tile(unsigned lin, int nimg, const Ti
     }
 }
 
-template <typename Coords, bool kVec, bool kStamp = false, int kNTPub = 1, int kUF = kSplatU, int kMap = 0>
+// What SPLAT writes.  Split engine: valid, collision and the winner map (the
+// workspace's); fused engine (kFuse): valid, collision and the C output
+// planes, gathered from obj right out of the LDS z-buffer.
+struct SplatIO {
+    float *valid, *coll;
+    const float *obj;  // kFuse only
+    float *out;        // kFuse only
+    int C;
+};
+
+template <typename Coords, bool kVec, bool kFuse = false, bool kStamp = false, int kNTPub = 1, int kUF = kSplatU,
+          int kMap = 0>
 __global__ __launch_bounds__(kWarpThreads, 8) void splat_kernel(Coords co, const float *__restrict__ depth,
-                                                                float *__restrict__ valid, float *__restrict__ coll,
-                                                                ChunkArgs a, int H, int W, int64_t HW, TileGeom g,
-                                                                unsigned long long *stamps = nullptr) {
+                                                                SplatIO io, ChunkArgs a, int H, int W, int64_t HW,
+                                                                TileGeom g, unsigned long long *stamps = nullptr) {
     __shared__ TileLds L;
     const unsigned total = unsigned(a.nimg) * unsigned(g.ntiles);
     const unsigned per = (total + 7u) / 8u;
@@ -595,29 +638,75 @@ __global__ __launch_bounds__(kWarpThreads, 8) void splat_kernel(Coords co, const
         __syncthreads();
     }
     if constexpr (kStamp) { if (threadIdx.x == 0) { ph[6] = wall_clock64(); ph[7] = L.nseg; } }
-    // ---- 5. publish: winner index, valid, collision (lane-consecutive rows)
-    unsigned int *win = ws.winner + int64_t(bl) * HW;
-    float *vb = valid + b * HW;
-    float *cb = coll + b * HW;
+    // ---- 5. publish (lane-consecutive rows of the tile)
+    float *vb = io.valid + b * HW;
+    float *cb = io.coll + b * HW;
+    if constexpr (kFuse) {
+        // valid, collision, and the winners' C channels: kT targets per thread
+        // with all their gathers in flight before any store.  The output
+        // planes and masks are touched once: non-temporal.
+        constexpr int kT = 2, kCh = 8;
+        const int C = io.C;
+        const float *ob = io.obj + b * int64_t(C) * HW;
+        float *oo = io.out + b * int64_t(C) * HW;
+        const unsigned uHW = unsigned(HW);
 #pragma unroll
-    for (int k = 0; k < TW * TH / kWarpThreads; ++k) {
-        const int q = int(threadIdx.x) + k * kWarpThreads;
-        const int ly = q / TW, lx = q - ly * TW;
-        const int ty = y0 + ly, tx = x0 + lx;
-        if (ty >= H || tx >= W) continue;
-        const unsigned long long key = L.zk[q];
-        const bool touched = key != KEY_UNTOUCHED;
-        const bool nowin = key == KEY_NOWIN;
-        const unsigned t = unsigned(ty) * unsigned(W) + unsigned(tx);
-        const unsigned wv = (touched && !nowin) ? unsigned(key & 0xFFFFFFFFull) : WIN_NONE;
-        if constexpr (kNTPub >= 2) __builtin_nontemporal_store(wv, win + t);
-        else win[t] = wv;
-        if constexpr (kNTPub >= 1) {
-            __builtin_nontemporal_store(touched ? 1.f : 0.f, vb + t);
-            __builtin_nontemporal_store(nowin ? 1.f : 0.f, cb + t);
-        } else {
-            vb[t] = touched ? 1.f : 0.f;
-            cb[t] = nowin ? 1.f : 0.f;
+        for (int k = 0; k < TW * TH / kWarpThreads; k += kT) {
+            unsigned t[kT], w[kT];
+            bool in[kT];
+#pragma unroll
+            for (int u = 0; u < kT; ++u) {
+                const int q = int(threadIdx.x) + (k + u) * kWarpThreads;
+                const int ly = q / TW, lx = q - ly * TW;
+                const int ty = y0 + ly, tx = x0 + lx;
+                in[u] = ty < H && tx < W;
+                const unsigned long long key = L.zk[q];
+                const bool touched = key != KEY_UNTOUCHED;
+                const bool nowin = key == KEY_NOWIN;
+                t[u] = unsigned(ty) * unsigned(W) + unsigned(tx);
+                w[u] = (in[u] && touched && !nowin) ? unsigned(key & 0xFFFFFFFFull) : WIN_NONE;
+                if (in[u]) {
+                    __builtin_nontemporal_store(touched ? 1.f : 0.f, vb + t[u]);
+                    __builtin_nontemporal_store(nowin ? 1.f : 0.f, cb + t[u]);
+                }
+            }
+            for (int c0 = 0; c0 < C; c0 += kCh) {
+                float o[kT][kCh];
+#pragma unroll
+                for (int u = 0; u < kT; ++u)
+#pragma unroll
+                    for (int cc = 0; cc < kCh; ++cc)
+                        o[u][cc] = (w[u] != WIN_NONE && c0 + cc < C) ? ob[unsigned(c0 + cc) * uHW + w[u]] : 0.f;
+#pragma unroll
+                for (int u = 0; u < kT; ++u)
+#pragma unroll
+                    for (int cc = 0; cc < kCh; ++cc)
+                        if (in[u] && c0 + cc < C)
+                            __builtin_nontemporal_store(o[u][cc], oo + unsigned(c0 + cc) * uHW + t[u]);
+            }
+        }
+    } else {
+        unsigned int *win = ws.winner + int64_t(bl) * HW;
+#pragma unroll
+        for (int k = 0; k < TW * TH / kWarpThreads; ++k) {
+            const int q = int(threadIdx.x) + k * kWarpThreads;
+            const int ly = q / TW, lx = q - ly * TW;
+            const int ty = y0 + ly, tx = x0 + lx;
+            if (ty >= H || tx >= W) continue;
+            const unsigned long long key = L.zk[q];
+            const bool touched = key != KEY_UNTOUCHED;
+            const bool nowin = key == KEY_NOWIN;
+            const unsigned t = unsigned(ty) * unsigned(W) + unsigned(tx);
+            const unsigned wv = (touched && !nowin) ? unsigned(key & 0xFFFFFFFFull) : WIN_NONE;
+            if constexpr (kNTPub >= 2) __builtin_nontemporal_store(wv, win + t);
+            else win[t] = wv;
+            if constexpr (kNTPub >= 1) {
+                __builtin_nontemporal_store(touched ? 1.f : 0.f, vb + t);
+                __builtin_nontemporal_store(nowin ? 1.f : 0.f, cb + t);
+            } else {
+                vb[t] = touched ? 1.f : 0.f;
+                cb[t] = nowin ? 1.f : 0.f;
+            }
         }
     }
     if constexpr (kStamp) {
@@ -790,16 +879,18 @@ int check_dims(int64_t B, int64_t C, int64_t H, int64_t W) {
     return OFD_FW_OK;
 }
 
-enum class Mode { Tile = 0, Atomic = 1 };
+enum class Mode { Tile = 0, Atomic = 1, TileSplit = 2 };
 
-// Engine selection: OFD_FW_MODE=atomic in the environment, or
-// ofd_fw_set_engine() at run time (tests and benchmarks compare the two).
+// Engine selection: OFD_FW_MODE=atomic|split in the environment, or
+// ofd_fw_set_engine() at run time (tests and benchmarks compare them).
 int g_engine = -1;
 
 Mode engine_mode() {
     if (g_engine < 0) {
         const char *e = getenv("OFD_FW_MODE");
-        g_engine = (e && strcmp(e, "atomic") == 0) ? int(Mode::Atomic) : int(Mode::Tile);
+        g_engine = (e && strcmp(e, "atomic") == 0)  ? int(Mode::Atomic)
+                   : (e && strcmp(e, "split") == 0) ? int(Mode::TileSplit)
+                                                    : int(Mode::Tile);
     }
     return Mode(g_engine);
 }
@@ -895,19 +986,33 @@ int run_f32(Coords co, const float *obj, const float *depth, float *out, float *
             if (c == nch - 1 && g_prof_stop) (void)hipEventRecord(g_prof_stop, st);
         } else {
             const ChunkArgs a{slab, b0, int(nb)};
+            const SplatIO io{valid, coll, obj, out, int(C)};
+            const dim3 bgrid(grid_for(nb * g.nseg, kWaves * kBinSPW));
             if (vec)
-                hipLaunchKernelGGL((bin_kernel<Coords, true>), dim3(grid_for(nb * g.nseg, kWaves)),
-                                   dim3(kWarpThreads), 0, st, co, depth, a, int(H), int(W), HW, g);
+                hipLaunchKernelGGL((bin_kernel<Coords, true, kBinSPW>), bgrid, dim3(kWarpThreads), 0, st, co, depth, a,
+                                   int(H), int(W), HW, g);
             else
-                hipLaunchKernelGGL((bin_kernel<Coords, false>), dim3(grid_for(nb * g.nseg, kWaves)),
-                                   dim3(kWarpThreads), 0, st, co, depth, a, int(H), int(W), HW, g);
-            const unsigned tiles = unsigned(nb * g.ntiles);
+                hipLaunchKernelGGL((bin_kernel<Coords, false, kBinSPW>), bgrid, dim3(kWarpThreads), 0, st, co, depth,
+                                   a, int(H), int(W), HW, g);
+            const dim3 sgrid((unsigned(nb * g.ntiles) + 7u) / 8u * 8u);
+            if (mode == Mode::Tile) {
+                // fused: SPLAT gathers the output planes itself (dominant kernel)
+                if (c == 0 && g_prof_start) (void)hipEventRecord(g_prof_start, st);
+                if (vec)
+                    hipLaunchKernelGGL((splat_kernel<Coords, true, true>), sgrid, dim3(kWarpThreads), 0, st, co,
+                                       depth, io, a, int(H), int(W), HW, g, nullptr);
+                else
+                    hipLaunchKernelGGL((splat_kernel<Coords, false, true>), sgrid, dim3(kWarpThreads), 0, st, co,
+                                       depth, io, a, int(H), int(W), HW, g, nullptr);
+                if (c == nch - 1 && g_prof_stop) (void)hipEventRecord(g_prof_stop, st);
+                continue;
+            }
             if (vec)
-                hipLaunchKernelGGL((splat_kernel<Coords, true>), dim3((tiles + 7u) / 8u * 8u), dim3(kWarpThreads), 0,
-                                   st, co, depth, valid, coll, a, int(H), int(W), HW, g, nullptr);
+                hipLaunchKernelGGL((splat_kernel<Coords, true>), sgrid, dim3(kWarpThreads), 0, st, co, depth, io, a,
+                                   int(H), int(W), HW, g, nullptr);
             else
-                hipLaunchKernelGGL((splat_kernel<Coords, false>), dim3((tiles + 7u) / 8u * 8u), dim3(kWarpThreads),
-                                   0, st, co, depth, valid, coll, a, int(H), int(W), HW, g, nullptr);
+                hipLaunchKernelGGL((splat_kernel<Coords, false>), sgrid, dim3(kWarpThreads), 0, st, co, depth, io, a,
+                                   int(H), int(W), HW, g, nullptr);
             const dim3 rgrid(unsigned((W + 64 * kResolveWX - 1) / (64 * kResolveWX)),
                              unsigned((H + kResolveRows - 1) / kResolveRows), unsigned(nb));
             const dim3 rblock(64 * kResolveWX * kResolveRows);
@@ -939,7 +1044,8 @@ int ofd_fw_set_profile_events(void *start_event, void *stop_event) {
 
 int ofd_fw_set_engine(int engine) {
     const int prev = int(engine_mode());
-    if (engine == OFD_FW_ENGINE_TILE || engine == OFD_FW_ENGINE_ATOMIC) g_engine = engine;
+    if (engine == OFD_FW_ENGINE_TILE || engine == OFD_FW_ENGINE_ATOMIC || engine == OFD_FW_ENGINE_TILE_SPLIT)
+        g_engine = engine;
     return prev;
 }
 

@@ -162,7 +162,7 @@ def test_repeatable_and_workspace_reuse(cuda_device):
     exp64 = oracle.forward_warping(o64, sy.astype(np.float64), sx.astype(np.float64), d64)
     prev = lib.ofd_fw_set_engine(0)
     try:
-        for engine in (0, 1, 0, 1):
+        for engine in (0, 1, 2, 0, 2, 1):
             lib.ofd_fw_set_engine(engine)
             got64 = fw_cuda.forward_warping(*(_t(x, cuda_device) for x in
                                               (o64, sy.astype(np.float64), sx.astype(np.float64), d64)))
@@ -270,18 +270,19 @@ def test_FW_3d_matches_batched(cuda_device):
         assert torch.equal(o, ob[i]) and torch.equal(v, vb[i]) and torch.equal(c, cb[i])
 
 
-# ------------------------------------------------------------------ both engines
-@pytest.fixture
-def atomic_engine():
+# ------------------------------------------------------------------ every engine
+# 0 = TILE (fused SPLAT gathers the output), 1 = ATOMIC, 2 = TILE_SPLIT (winner map + RESOLVE)
+@pytest.fixture(params=[1, 2], ids=["atomic", "split"])
+def other_engine(request):
     from opticalflowfromdepth_amd import _native
     lib = _native.lib()
-    prev = lib.ofd_fw_set_engine(1)
-    yield
+    prev = lib.ofd_fw_set_engine(request.param)
+    yield request.param
     lib.ofd_fw_set_engine(prev)
 
 
 @pytest.mark.parametrize("seed", range(4))
-def test_atomic_engine_random_vs_oracle(cuda_device, atomic_engine, seed):
+def test_other_engines_random_vs_oracle(cuda_device, other_engine, seed):
     from opticalflowfromdepth_amd import forward_warp_flow
     rng = np.random.default_rng(100 + seed)
     B, C, H, W = 3, int(rng.choice([2, 6, 7])), int(rng.integers(5, 90)), int(rng.integers(5, 120))
@@ -289,7 +290,7 @@ def test_atomic_engine_random_vs_oracle(cuda_device, atomic_engine, seed):
     flow = (rng.standard_normal((B, 2, H, W)) * rng.uniform(0.1, 60)).astype(np.float32)
     depth = rng.integers(0, 4, (B, 1, H, W)).astype(np.float32)
     got = forward_warp_flow(_t(obj, cuda_device), _t(flow, cuda_device), _t(depth, cuda_device))
-    _assert_same(got, oracle.fw_flow(obj, flow, depth), f"atomic seed{seed}")
+    _assert_same(got, oracle.fw_flow(obj, flow, depth), f"engine {other_engine} seed{seed}")
 
 
 def test_engines_agree_on_realistic_batch(cuda_device):
@@ -299,12 +300,13 @@ def test_engines_agree_on_realistic_batch(cuda_device):
     prev = lib.ofd_fw_set_engine(0)
     try:
         a = forward_warp_flow(obj, flow, depth)
-        lib.ofd_fw_set_engine(1)
-        b = forward_warp_flow(obj, flow, depth)
+        for engine in (1, 2):
+            lib.ofd_fw_set_engine(engine)
+            b = forward_warp_flow(obj, flow, depth)
+            for x, y in zip(a, b):
+                assert torch.equal(x, y), engine
     finally:
         lib.ofd_fw_set_engine(prev)
-    for x, y in zip(a, b):
-        assert torch.equal(x, y)
 
 
 def test_tile_engine_overflow_and_wide_boxes(cuda_device):

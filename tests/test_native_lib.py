@@ -57,7 +57,8 @@ def test_engine_switch():
     cur = lib.ofd_fw_set_engine(-1)
     assert cur in (0, 1)
     assert lib.ofd_fw_set_engine(1) == cur
-    assert lib.ofd_fw_set_engine(0) == 1
+    assert lib.ofd_fw_set_engine(2) == 1
+    assert lib.ofd_fw_set_engine(0) == 2
     lib.ofd_fw_set_engine(cur)
 
 

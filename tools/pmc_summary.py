@@ -35,9 +35,11 @@ def main():
     f = per_dispatch(fd)
     w = per_dispatch(wd)
     names = [x[0] for x in f]
-    per_call = 3 if "bin_kernel" in names else 2  # tile engine: BIN, SPLAT, RESOLVE
+    # launches per call: BIN + SPLAT (tile), + RESOLVE (split), or the atomic pair
+    per_call = len(set(names))
     f, w = f[-per_call:], w[-per_call:]
-    rep = {"config": [B, C, H, W], "kernels": []}
+    engine = ("split" if "resolve2d_kernel" in names else "tile" if "bin_kernel" in names else "atomic")
+    rep = {"config": [B, C, H, W], "engine": engine, "kernels": []}
     tot_r = tot_w = 0.0
     for (n, fk, t), (_, wk, _) in zip(f, w):
         rb, wb = fk * 1024 * 2, wk * 1024   # KiB; FETCH x2 on gfx950
