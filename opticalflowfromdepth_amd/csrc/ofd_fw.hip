@@ -65,7 +65,11 @@ constexpr unsigned long long ZKEY_NOWIN = ~0ull - 1ull;
 constexpr unsigned int IDX_NONE = ~0u;
 
 // tile engine geometry
-constexpr int TW = 128, TH = 32;          // target tile (LDS z-buffer 32 KiB)
+#ifndef OFD_PROBE_TW  // tile shape: overridable only by the diagnostic probe build (tools/probe_tile.py)
+#define OFD_PROBE_TW 128
+#define OFD_PROBE_TH 32
+#endif
+constexpr int TW = OFD_PROBE_TW, TH = OFD_PROBE_TH;  // target tile (LDS z-buffer 32 KiB)
 constexpr int SBW = 16, SBH = 4;          // source block = one wave (64 px)
 constexpr int SEGB = 8;                   // source blocks per segment (128 x 4 px)
 constexpr int MAX_TILES_PER_BLOCK = 12;   // wider boxes go through the global path
@@ -186,6 +190,16 @@ struct FlowCoords {  // FW.forward input: flow [B,2,H,W], ch0 = x, ch1 = y
 // ---------------------------------------------------------------- wave helpers
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS
+// operations (lgkmcnt), not for its outstanding global loads and stores --
+// __syncthreads() would also drain every store, e.g. a tile's published
+// output before the next tile of a persistent loop may start.
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // Packed min of two unsigned 16-bit halves (one v_pk_min_u16).
 __device__ __forceinline__ unsigned pk_min_u16(unsigned a, unsigned b) {
     unsigned r;
@@ -243,10 +257,11 @@ inline size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
 // Per-image workspace: key slab (HW u64, only touched by spills), winner map
 // (HW u32), per-tile spill flags, and the target-tile boxes of every source
-// segment and block.
+// segment and block; plus, once per chunk slab, the persistent SPLAT's tile
+// queue words (inside the per-image slack).
 inline size_t per_image_bytes(int64_t H, int64_t W) {
     const TileGeom g = make_geom(H, W);
-    return size_t(H) * size_t(W) * 12 + size_t(g.ntiles) * 4 + size_t(g.nseg) * 8 + size_t(g.nsb) * 8 + 64;
+    return size_t(H) * size_t(W) * 12 + size_t(g.ntiles) * 4 + size_t(g.nseg) * 8 + size_t(g.nsb) * 8 + 256;
 }
 
 struct Ws {  // views of one chunk's workspace (G images)
@@ -255,6 +270,7 @@ struct Ws {  // views of one chunk's workspace (G images)
     unsigned int *flag;        // [G][ntiles]  0 = merge key slab, ~0 = clean
     ushort4 *segrec;           // [G][nseg]    scratch: target tile box (t0x,t1x,t0y,t1y) of a segment
     ushort4 *blkrec;           // [G][nsb]     scratch: same per source block
+    unsigned int *queue;       // [16]         persistent SPLAT: 8 per-XCD tile queues + exit count, ~0 between calls
 };
 
 inline Ws carve(void *ws, int64_t G, int64_t HW, const TileGeom &g) {
@@ -269,6 +285,8 @@ inline Ws carve(void *ws, int64_t G, int64_t HW, const TileGeom &g) {
     w.segrec = reinterpret_cast<ushort4 *>(p);
     p += align16(size_t(G) * g.nseg * 8);
     w.blkrec = reinterpret_cast<ushort4 *>(p);
+    p += align16(size_t(G) * g.nsb * 8);
+    w.queue = reinterpret_cast<unsigned int *>(p);
     return w;
 }
 
@@ -311,6 +329,7 @@ struct TileLds {
     unsigned int seg[kSegCap];
     unsigned int blk[kListCap];
     unsigned int nseg, nblk, flag;
+    unsigned int next;  // persistent SPLAT: the tile thread 0 dequeued
 };
 
 struct ChunkArgs {  // one chunk of images
@@ -480,24 +499,30 @@ struct SplatIO {
     int C;
 };
 
-template <typename Coords, bool kVec, bool kFuse = false, bool kStamp = false, int kNTPub = 1, int kUF = kSplatU,
-          int kMap = 0>
-__global__ __launch_bounds__(kWarpThreads, 8) void splat_kernel(Coords co, const float *__restrict__ depth,
-                                                                SplatIO io, ChunkArgs a, int H, int W, int64_t HW,
-                                                                TileGeom g, unsigned long long *stamps = nullptr) {
-    __shared__ TileLds L;
-    const unsigned total = unsigned(a.nimg) * unsigned(g.ntiles);
-    const unsigned per = (total + 7u) / 8u;
-    const unsigned lin = (blockIdx.x % 8u) * per + blockIdx.x / 8u;
-    if (lin >= total) return;
+// SPLAT launch shape: threads per workgroup, gather targets in flight per
+// thread (fused publish), minimum waves per SIMD (__launch_bounds__), 4-block
+// slots in flight per wave, publish store policy, tile order (probe knobs).
+template <int kThr_, int kGT_, int kMinW_, int kUF_ = kSplatU, int kNTPub_ = 1, int kMap_ = 0>
+struct SplatCfg {
+    static constexpr int kThr = kThr_, kWaves = kThr_ / 64, kGT = kGT_, kMinW = kMinW_, kUF = kUF_, kNTPub = kNTPub_,
+                         kMap = kMap_;
+};
+
+// One target tile (linear index `lin` of the chunk's band-major tile order).
+// Every barrier is LDS-only: global loads are consumed by the thread that
+// issued them, and the published stores are never waited for.
+template <typename Coords, bool kVec, bool kFuse, bool kStamp, typename Cfg>
+__device__ __forceinline__ void splat_tile(TileLds &L, unsigned lin, const Coords &co, const float *__restrict__ depth,
+                                           const SplatIO &io, const ChunkArgs &a, int H, int W, int64_t HW,
+                                           const TileGeom &g, unsigned long long *stamps) {
     unsigned long long *ph = kStamp ? stamps + 8 * lin : nullptr;
     if constexpr (kStamp) { if (threadIdx.x == 0) ph[0] = wall_clock64(); }
 
     const Ws &ws = a.ws;
     int bl, tile;
-    if constexpr (kMap == 0) {
+    if constexpr (Cfg::kMap == 0) {
         band_major_tile(lin, a.nimg, g, bl, tile);
-    } else if constexpr (kMap == 1) {  // whole images, image k, k+8, ... on XCD k
+    } else if constexpr (Cfg::kMap == 1) {  // whole images, image k, k+8, ... on XCD k
         const unsigned s0 = lin / unsigned(g.ntiles);
         tile = int(lin - s0 * unsigned(g.ntiles));
         const unsigned nq = unsigned(a.nimg) / 8u, nr = unsigned(a.nimg) % 8u;
@@ -523,26 +548,26 @@ __global__ __launch_bounds__(kWarpThreads, 8) void splat_kernel(Coords co, const
         L.nseg = 0;
         L.nblk = 0;
     }
-    for (int k = threadIdx.x; k < TW * TH; k += kWarpThreads) L.zk[k] = KEY_UNTOUCHED;
-    __syncthreads();
+    for (int k = threadIdx.x; k < TW * TH; k += Cfg::kThr) L.zk[k] = KEY_UNTOUCHED;
+    lds_barrier();
 
     // ---- 1. segments whose box holds this tile (all loads of a thread in flight together)
-    for (int s0 = threadIdx.x; s0 < g.nseg; s0 += kWarpThreads * 4) {
+    for (int s0 = threadIdx.x; s0 < g.nseg; s0 += Cfg::kThr * 4) {
         ushort4 r[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            const int sidx = s0 + u * kWarpThreads;
+            const int sidx = s0 + u * Cfg::kThr;
             r[u] = sidx < g.nseg ? segrec[sidx] : empty_box();
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             if (box_has(r[u], txi, tyi)) {
                 const unsigned idx = atomicAdd(&L.nseg, 1u);
-                if (idx < unsigned(kSegCap)) L.seg[idx] = unsigned(s0 + u * kWarpThreads);
+                if (idx < unsigned(kSegCap)) L.seg[idx] = unsigned(s0 + u * Cfg::kThr);
             }
         }
     }
-    __syncthreads();
+    lds_barrier();
     if constexpr (kStamp) { if (threadIdx.x == 0) ph[4] = wall_clock64(); }
     const int nsel = int(L.nseg);
     // candidates: the blocks of the selected segments, or every block of the
@@ -554,8 +579,8 @@ __global__ __launch_bounds__(kWarpThreads, 8) void splat_kernel(Coords co, const
     for (int c0 = 0; c0 < ncand; c0 += kListCap) {
         // ---- 2. candidate blocks whose box holds this tile -> L.blk
 #pragma unroll
-        for (int u = 0; u < kListCap / kWarpThreads; ++u) {
-            const int c = c0 + int(threadIdx.x) + u * kWarpThreads;
+        for (int u = 0; u < kListCap / Cfg::kThr; ++u) {
+            const int c = c0 + int(threadIdx.x) + u * Cfg::kThr;
             int sb = -1;
             if (c < ncand) {
                 if (all_blocks) {
@@ -571,21 +596,21 @@ __global__ __launch_bounds__(kWarpThreads, 8) void splat_kernel(Coords co, const
                 L.blk[idx] = unsigned(sb);
             }
         }
-        __syncthreads();
+        lds_barrier();
         // ---- 3. splat the selected blocks into the LDS z-buffer.  A slot is 4
         // blocks: lane = (block lane/16, row (lane/4)%4, pixels 4*(lane%4)..+3),
         // one 16-byte load per plane (kVec); kU slots in flight per wave.
         using V = typename Coords::V;
-        constexpr int kU = sizeof(V) == 4 ? kUF : 1;  // 64-VGPR budget
+        constexpr int kU = sizeof(V) == 4 ? Cfg::kUF : 1;  // 64-VGPR budget
         const int nb = int(L.nblk);
         const int sub = lane >> 4, rr = (lane >> 2) & 3, c4 = (lane & 3) * 4;
-        for (int e0 = wave * 4; e0 < nb; e0 += kWaves * 4 * kU) {
+        for (int e0 = wave * 4; e0 < nb; e0 += Cfg::kWaves * 4 * kU) {
             V cx[kU][4], cy[kU][4];
             float d[kU][4];
             int ii[kU], jj[kU];
 #pragma unroll
             for (int u = 0; u < kU; ++u) {
-                const int e = e0 + sub + u * kWaves * 4;
+                const int e = e0 + sub + u * Cfg::kWaves * 4;
                 ii[u] = W;
                 jj[u] = 0;
                 if (e < nb) {
@@ -616,14 +641,14 @@ __global__ __launch_bounds__(kWarpThreads, 8) void splat_kernel(Coords co, const
                 }
             }
         }
-        __syncthreads();
+        lds_barrier();
         if (threadIdx.x == 0) L.nblk = 0;
-        __syncthreads();
+        lds_barrier();
     }
     if constexpr (kStamp) { if (threadIdx.x == 0) ph[5] = wall_clock64(); }
     // ---- 4. merge the key slab where BIN spilled into it
     if (L.flag == 0u) {
-        for (int k = threadIdx.x; k < TW * TH; k += kWarpThreads) {
+        for (int k = threadIdx.x; k < TW * TH; k += Cfg::kThr) {
             const int ly = k / TW, lx = k - ly * TW;
             const int tx = x0 + lx, ty = y0 + ly;
             if (tx < W && ty < H) {
@@ -635,7 +660,7 @@ __global__ __launch_bounds__(kWarpThreads, 8) void splat_kernel(Coords co, const
                 }
             }
         }
-        __syncthreads();
+        lds_barrier();
     }
     if constexpr (kStamp) { if (threadIdx.x == 0) { ph[6] = wall_clock64(); ph[7] = L.nseg; } }
     // ---- 5. publish (lane-consecutive rows of the tile)
@@ -645,18 +670,18 @@ __global__ __launch_bounds__(kWarpThreads, 8) void splat_kernel(Coords co, const
         // valid, collision, and the winners' C channels: kT targets per thread
         // with all their gathers in flight before any store.  The output
         // planes and masks are touched once: non-temporal.
-        constexpr int kT = 2, kCh = 8;
+        constexpr int kT = Cfg::kGT, kCh = 8;
         const int C = io.C;
         const float *ob = io.obj + b * int64_t(C) * HW;
         float *oo = io.out + b * int64_t(C) * HW;
         const unsigned uHW = unsigned(HW);
 #pragma unroll
-        for (int k = 0; k < TW * TH / kWarpThreads; k += kT) {
+        for (int k = 0; k < TW * TH / Cfg::kThr; k += kT) {
             unsigned t[kT], w[kT];
             bool in[kT];
 #pragma unroll
             for (int u = 0; u < kT; ++u) {
-                const int q = int(threadIdx.x) + (k + u) * kWarpThreads;
+                const int q = int(threadIdx.x) + (k + u) * Cfg::kThr;
                 const int ly = q / TW, lx = q - ly * TW;
                 const int ty = y0 + ly, tx = x0 + lx;
                 in[u] = ty < H && tx < W;
@@ -688,8 +713,8 @@ __global__ __launch_bounds__(kWarpThreads, 8) void splat_kernel(Coords co, const
     } else {
         unsigned int *win = ws.winner + int64_t(bl) * HW;
 #pragma unroll
-        for (int k = 0; k < TW * TH / kWarpThreads; ++k) {
-            const int q = int(threadIdx.x) + k * kWarpThreads;
+        for (int k = 0; k < TW * TH / Cfg::kThr; ++k) {
+            const int q = int(threadIdx.x) + k * Cfg::kThr;
             const int ly = q / TW, lx = q - ly * TW;
             const int ty = y0 + ly, tx = x0 + lx;
             if (ty >= H || tx >= W) continue;
@@ -698,9 +723,9 @@ __global__ __launch_bounds__(kWarpThreads, 8) void splat_kernel(Coords co, const
             const bool nowin = key == KEY_NOWIN;
             const unsigned t = unsigned(ty) * unsigned(W) + unsigned(tx);
             const unsigned wv = (touched && !nowin) ? unsigned(key & 0xFFFFFFFFull) : WIN_NONE;
-            if constexpr (kNTPub >= 2) __builtin_nontemporal_store(wv, win + t);
+            if constexpr (Cfg::kNTPub >= 2) __builtin_nontemporal_store(wv, win + t);
             else win[t] = wv;
-            if constexpr (kNTPub >= 1) {
+            if constexpr (Cfg::kNTPub >= 1) {
                 __builtin_nontemporal_store(touched ? 1.f : 0.f, vb + t);
                 __builtin_nontemporal_store(nowin ? 1.f : 0.f, cb + t);
             } else {
@@ -710,8 +735,72 @@ __global__ __launch_bounds__(kWarpThreads, 8) void splat_kernel(Coords co, const
         }
     }
     if constexpr (kStamp) {
-        __syncthreads();
+        lds_barrier();
         if (threadIdx.x == 0) { ph[1] = wall_clock64(); ph[2] = 0; ph[3] = lin; }
+    }
+}
+
+using SplitCfg = SplatCfg<512, 2, 8>;  // split engine: 4 workgroups / CU, light publish
+// fused engine: 2 workgroups / CU (VGPR-bound), every target's gathers of a
+// thread (8 x C) in flight at once.  Measured at 64 x 768x1024, C = 6
+// (tools/probe_tile.py): 512 threads / 2 in flight / 4 per CU 702 us;
+// 512 / 8 / 2 per CU 675; as a persistent kernel 655; 256 threads 715.
+using FusedCfg = SplatCfg<512, 8, 4>;
+
+template <typename Coords, bool kVec, bool kFuse = false, bool kStamp = false, typename Cfg = SplitCfg>
+__global__ __launch_bounds__(Cfg::kThr, Cfg::kMinW) void splat_kernel(Coords co, const float *__restrict__ depth,
+                                                                SplatIO io, ChunkArgs a, int H, int W, int64_t HW,
+                                                                TileGeom g, unsigned long long *stamps = nullptr) {
+    __shared__ TileLds L;
+    const unsigned total = unsigned(a.nimg) * unsigned(g.ntiles);
+    const unsigned per = (total + 7u) / 8u;
+    const unsigned lin = (blockIdx.x % 8u) * per + blockIdx.x / 8u;
+    if (lin >= total) return;
+    splat_tile<Coords, kVec, kFuse, kStamp, Cfg>(L, lin, co, depth, io, a, H, W, HW, g, stamps);
+}
+
+// Persistent SPLAT: one workgroup per resident slot, looping over tiles.  The
+// band-major tile order is cut into 8 contiguous queues, queue k served first
+// by the workgroups with blockIdx % 8 == k (one XCD under round-robin
+// placement); a workgroup whose queue is drained takes tiles from the next
+// queues.  Queue words count down from ~0 (the workspace's initial state);
+// the last workgroup out restores them, so the next launch starts clean.
+// Placement and order affect speed only: every tile is processed exactly
+// once, and no workgroup ever waits for another.
+template <typename Coords, bool kVec, bool kFuse = true, bool kStamp = false, typename Cfg = FusedCfg>
+__global__ __launch_bounds__(Cfg::kThr, Cfg::kMinW) void splat_persist_kernel(Coords co, const float *__restrict__ depth,
+                                                                        SplatIO io, ChunkArgs a, int H, int W,
+                                                                        int64_t HW, TileGeom g,
+                                                                        unsigned long long *stamps = nullptr) {
+    __shared__ TileLds L;
+    unsigned *queue = a.ws.queue;
+    const unsigned total = unsigned(a.nimg) * unsigned(g.ntiles);
+    const unsigned per = (total + 7u) / 8u;
+    const unsigned home = blockIdx.x % 8u;
+    unsigned drained = 0;  // thread 0: queues seen empty
+    for (;;) {
+        if (threadIdx.x == 0) {
+            unsigned lin = ~0u;
+            for (unsigned k = 0; k < 8u && lin == ~0u; ++k) {
+                const unsigned qx = (home + k) & 7u;
+                if ((drained >> qx) & 1u) continue;
+                const unsigned idx = ~atomicSub(queue + qx, 1u);
+                const unsigned l = qx * per + idx;
+                if (idx < per && l < total) lin = l;
+                else drained |= 1u << qx;
+            }
+            if (lin == ~0u && ~atomicSub(queue + 8, 1u) == gridDim.x - 1u) {
+                // every other workgroup has finished dequeuing: restore the queues
+                for (int k = 0; k < 9; ++k) atomicExch(queue + k, ~0u);
+            }
+            L.next = lin;
+        }
+        lds_barrier();
+        const unsigned lin = L.next;
+        if (lin == ~0u) return;
+        splat_tile<Coords, kVec, kFuse, kStamp, Cfg>(L, lin, co, depth, io, a, H, W, HW, g, stamps);
+        // splat_tile ends with LDS reads of the z-buffer; the next iteration's
+        // barrier orders them before the next tile's initialisation
     }
 }
 
@@ -939,6 +1028,26 @@ bool claim_layout(const void *ws, const LayoutSig &sig) {
     return !ok;
 }
 
+// Resident workgroup slots of a kernel on the current device (the persistent
+// SPLAT's grid); queried once per kernel instantiation.
+template <typename K>
+unsigned resident_slots(K kernel, int threads) {
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void *>(kernel), threads, 0) !=
+            hipSuccess ||
+        cus <= 0 || per <= 0)
+        return 1024u;
+    return unsigned(cus) * unsigned(per);
+}
+
+template <typename Coords, bool kVec, typename Cfg = FusedCfg>
+unsigned persist_grid(unsigned tiles) {
+    static const unsigned slots = resident_slots(splat_persist_kernel<Coords, kVec, true, false, Cfg>, Cfg::kThr);
+    return tiles < slots ? tiles : slots;
+}
+
 // Optional timing hook (ofd_fw_set_profile_events): events recorded on the
 // launch stream right before the first and right after the last RESOLVE
 // launch of a call -- the dominant kernel -- so a benchmark can time it with
@@ -996,14 +1105,15 @@ int run_f32(Coords co, const float *obj, const float *depth, float *out, float *
                                    a, int(H), int(W), HW, g);
             const dim3 sgrid((unsigned(nb * g.ntiles) + 7u) / 8u * 8u);
             if (mode == Mode::Tile) {
-                // fused: SPLAT gathers the output planes itself (dominant kernel)
+                // fused: a persistent SPLAT gathers the output planes itself (dominant kernel)
+                const unsigned tiles = unsigned(nb * g.ntiles);
                 if (c == 0 && g_prof_start) (void)hipEventRecord(g_prof_start, st);
                 if (vec)
-                    hipLaunchKernelGGL((splat_kernel<Coords, true, true>), sgrid, dim3(kWarpThreads), 0, st, co,
-                                       depth, io, a, int(H), int(W), HW, g, nullptr);
+                    hipLaunchKernelGGL((splat_persist_kernel<Coords, true>), dim3(persist_grid<Coords, true>(tiles)),
+                                       dim3(FusedCfg::kThr), 0, st, co, depth, io, a, int(H), int(W), HW, g, nullptr);
                 else
-                    hipLaunchKernelGGL((splat_kernel<Coords, false, true>), sgrid, dim3(kWarpThreads), 0, st, co,
-                                       depth, io, a, int(H), int(W), HW, g, nullptr);
+                    hipLaunchKernelGGL((splat_persist_kernel<Coords, false>), dim3(persist_grid<Coords, false>(tiles)),
+                                       dim3(FusedCfg::kThr), 0, st, co, depth, io, a, int(H), int(W), HW, g, nullptr);
                 if (c == nch - 1 && g_prof_stop) (void)hipEventRecord(g_prof_stop, st);
                 continue;
             }

@@ -9,8 +9,14 @@
 
 // which:  0 / 3 / 4 = BIN with 1 / 2 / 4 segments per wave
 //         1 = SPLAT, split engine (stamped)       5 = SPLAT, split engine
-//         6 = SPLAT, fused engine (stamped)       7 = SPLAT, fused engine
+//         6 = SPLAT, fused engine (stamped)       7 = SPLAT, fused engine (product FusedCfg)
+//         8 = persistent fused SPLAT (stamped)    9 = persistent fused SPLAT
+//        10..14 = fused SPLAT launch-shape variants (see the cases)
 //         2 = RESOLVE (product shape)
+using C256 = SplatCfg<256, 8, 4>;
+using C512u3 = SplatCfg<512, 8, 4, 3>;
+using C256u3 = SplatCfg<256, 8, 4, 3>;
+
 extern "C" int probe_launch(int which, const float *obj, const float *flow, const float *depth, float *out,
                             float *valid, float *coll, int64_t C, int64_t H, int64_t W, void *slab, int64_t b0,
                             int nimg, unsigned long long *stamps, void *stream) {
@@ -34,10 +40,27 @@ extern "C" int probe_launch(int which, const float *obj, const float *flow, cons
                                int(W), HW, g, stamps); break;
     case 5: hipLaunchKernelGGL((splat_kernel<Co, true, false, false>), sgrid, blk, 0, st, co, depth, io, a, int(H),
                                int(W), HW, g, nullptr); break;
-    case 6: hipLaunchKernelGGL((splat_kernel<Co, true, true, true>), sgrid, blk, 0, st, co, depth, io, a, int(H),
-                               int(W), HW, g, stamps); break;
-    case 7: hipLaunchKernelGGL((splat_kernel<Co, true, true, false>), sgrid, blk, 0, st, co, depth, io, a, int(H),
-                               int(W), HW, g, nullptr); break;
+    case 6: hipLaunchKernelGGL((splat_kernel<Co, true, true, true, FusedCfg>), sgrid, blk, 0, st, co, depth, io, a,
+                               int(H), int(W), HW, g, stamps); break;
+    case 7: hipLaunchKernelGGL((splat_kernel<Co, true, true, false, FusedCfg>), sgrid, blk, 0, st, co, depth, io, a,
+                               int(H), int(W), HW, g, nullptr); break;
+    case 8: hipLaunchKernelGGL((splat_persist_kernel<Co, true, true, true>), dim3(persist_grid<Co, true>(sgrid.x)),
+                               blk, 0, st, co, depth, io, a, int(H), int(W), HW, g, stamps); break;
+    case 9: hipLaunchKernelGGL((splat_persist_kernel<Co, true, true, false>), dim3(persist_grid<Co, true>(sgrid.x)),
+                               blk, 0, st, co, depth, io, a, int(H), int(W), HW, g, nullptr); break;
+#define FV(CFG) hipLaunchKernelGGL((splat_kernel<Co, true, true, false, CFG>), sgrid, dim3(CFG::kThr), 0, st, co, depth, \
+                                   io, a, int(H), int(W), HW, g, nullptr)
+    case 10: FV(SplitCfg); break;                      // 512 threads, 2 targets in flight, 4 WG / CU
+    case 11: FV(C256); break;    // 256 threads, 8 in flight, LDS-bound 4 WG / CU
+    case 13: FV(C512u3); break;  // + 3 splat slots per wave
+    case 14: FV(C256u3); break;
+#undef FV
+    case 12: {
+        using P = SplatCfg<256, 8, 4>;
+        hipLaunchKernelGGL((splat_persist_kernel<Co, true, true, false, P>), dim3(persist_grid<Co, true, P>(sgrid.x)),
+                           dim3(P::kThr), 0, st, co, depth, io, a, int(H), int(W), HW, g, nullptr);
+        break;
+    }
     case 2:
         hipLaunchKernelGGL((resolve2d_kernel<8, kResolveRows, kResolveWX, true, true>),
                            dim3(unsigned((W + 64 * kResolveWX - 1) / (64 * kResolveWX)),

@@ -4,7 +4,8 @@ Builds tools/probe_tile.hip (the product TU + stamps), makes the headline
 workload with opticalflowfromdepth_amd.synth and times, interleaved over
 rounds, each launch of:
   split : BIN (1 segment / wave) -> SPLAT (winner map) -> RESOLVE
-  fused : BIN (1, 2, 4 segments / wave) -> SPLAT gathering the output itself
+  fused : BIN -> SPLAT gathering the output itself (one workgroup per tile)
+  persist: BIN -> the same SPLAT as a persistent kernel over per-XCD tile queues
 Prints per-launch medians, the SPLAT workgroups' phase medians (stamped
 builds) and checks every variant's result against the product library.
 """
@@ -20,12 +21,15 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 from opticalflowfromdepth_amd import _native, forward_warp_flow, synth  # noqa: E402
 
-SO = os.path.join(REPO, "tools", "_build", "libprobe_tile.so")
+SO = os.environ.get("PROBE_LIB") or os.path.join(REPO, "tools", "_build", "libprobe_tile.so")
 NAMES = {0: "bin1", 3: "bin2", 4: "bin4", 1: "splat(stamped)", 5: "splat", 6: "fused(stamped)", 7: "fused",
-         2: "resolve"}
+         8: "persist(stamped)", 9: "persist", 10: "fused512_t2w8", 11: "fused256_t8w4", 12: "persist256_t8w4",
+         13: "fused512_t8w4u3", 14: "fused256_t8w4u3", 2: "resolve"}
 
 
 def build():
+    if os.environ.get("PROBE_LIB"):
+        return  # a prebuilt variant (e.g. another tile shape)
     srcs = [os.path.join(REPO, "tools", "probe_tile.hip"), os.path.join(REPO, "opticalflowfromdepth_amd", "csrc",
                                                                        "ofd_fw.hip")]
     if os.path.exists(SO) and all(os.path.getmtime(SO) > os.path.getmtime(x) for x in srcs):
@@ -65,7 +69,7 @@ def main():
     C = obj.shape[1]
     out, valid, coll = torch.empty_like(obj), torch.empty_like(depth), torch.empty_like(depth)
     slab = torch.full((lib.probe_slab_bytes(B, H, W),), 255, dtype=torch.uint8, device=dev)
-    stamps = torch.zeros(8 * (B * 192 + 64), dtype=torch.int64, device=dev)
+    stamps = torch.zeros(8 * (B * 768 + 64), dtype=torch.int64, device=dev)
     st = torch.cuda.current_stream().cuda_stream
     base = (obj.data_ptr(), flow.data_ptr(), depth.data_ptr(), out.data_ptr(), valid.data_ptr(), coll.data_ptr(),
             C, H, W, slab.data_ptr(), 0, B, stamps.data_ptr(), st)
@@ -94,7 +98,8 @@ def main():
             t.fill_(-7.0)
         return ok
 
-    configs = {"split": [0, 5, 2], "fused/bin1": [0, 7], "fused/bin2": [3, 7], "fused/bin4": [4, 7]}
+    configs = {"split": [0, 5, 2], "fused": [0, 7], "persist": [0, 9], "f512t2": [0, 10], "f256t8": [0, 11],
+               "p256t8": [0, 12], "f512u3": [0, 13], "f256u3": [0, 14]}
     for name, whichs in configs.items():
         seq(whichs)
         check(name)
@@ -106,7 +111,7 @@ def main():
         med = np.median(np.array(times[name]), axis=0)
         print(f"{name:12s} " + "  ".join(f"{NAMES[w]}={m:6.1f}" for w, m in zip(whichs, med)) +
               f"  sum={med.sum():6.1f} us")
-    for label, whichs in (("split SPLAT", [0, 1]), ("fused SPLAT", [3, 6])):
+    for label, whichs in (("split SPLAT", [0, 1]), ("fused SPLAT", [0, 6]), ("persistent fused SPLAT", [0, 8])):
         stamps.zero_()
         seq(whichs)
         phases(stamps, label)
