@@ -166,7 +166,7 @@ def main():
     #           (BIN's flow read is the one re-read)
     #   split : RESOLVE gathers obj and writes the C output planes, 2C*4
     #   atomic: the resolve pass also writes valid / collision, (2C+2)*4
-    kern_bpp, kern_name = {"tile": ((2 * C + 5) * 4, "splat_kernel"),
+    kern_bpp, kern_name = {"tile": ((2 * C + 5) * 4, "splat_persist_kernel"),
                            "split": (2 * C * 4, "resolve2d_kernel"),
                            "atomic": ((2 * C + 2) * 4, "resolve_atomic_kernel")}[args.engine]
     kern_gbs = px_step_rank * kern_bpp / (resolve_ms / 1e3) / 1e9

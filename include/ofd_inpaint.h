@@ -1,0 +1,52 @@
+/*
+ * ofd_inpaint.h -- C ABI of the MI355X hole-fill (layered Telea inpainting).
+ *
+ * Same conventions as ofd_fw.h: plain pointers and sizes, gfx950 device
+ * pointers, dense contiguous NCHW float32, asynchronous on `stream` (a
+ * hipStream_t passed as void*, NULL = the legacy default stream); return 0 or
+ * an OFD_FW_E* code (< 0) or a hipError_t (> 0), named by ofd_fw_strerror().
+ *
+ * Entry point -> reference interface it replaces (AegeanKI/OpticalFlowFromDepth
+ * @ 2024_08_07):
+ *
+ *   ofd_inpaint_telea_f32
+ *       utils.inpaint(img, valid, collision)  -- utils.py:136-151, batched:
+ *       the keep-mask algebra of :137-142 (exact), the uint8 cast of :148, and
+ *       cv2.inpaint(img_u8, 1 - H', 3, cv2.INPAINT_TELEA) of :149 replaced by a
+ *       level-synchronous Telea fill (DESIGN.md "Hole-fill"): the same Telea
+ *       weights and fast-marching update, with holes finalised in layers of
+ *       equal L1 distance to the known region instead of one at a time.  The
+ *       fill values are therefore not cv2's (parity with cv2 is unpinned: no
+ *       OpenCV in the build image); the kernel is bit-exact against its CPU
+ *       restatement oracle/inpaint_oracle.c (layered mode).
+ *   ofd_inpaint_workspace_bytes
+ *       no reference counterpart (cv2 allocates its fast-marching state per
+ *       call); caller-owned scratch, no initialisation needed.
+ */
+#ifndef OFD_INPAINT_H
+#define OFD_INPAINT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Bytes of workspace for a call over B images of H x W (any size of at least
+ * one image's share works; larger workspaces process more images per launch). */
+size_t ofd_inpaint_workspace_bytes(int64_t B, int64_t H, int64_t W);
+
+/* utils.inpaint, batched.  img / out [B,C,H,W] f32 (out holds uint8 values),
+ * valid / collision [B,1,H,W] f32.  radius = cv2 inpaintRange (3 in the
+ * reference), clamped to [1, 100].  Requires H >= 2, W >= 2 (OFD_FW_EINVAL)
+ * and H + W <= 8192 (OFD_FW_ETOOBIG).  out must not alias img. */
+int ofd_inpaint_telea_f32(const float *img, const float *valid, const float *collision, float *out,
+                          int64_t B, int64_t C, int64_t H, int64_t W, int radius, void *workspace,
+                          size_t workspace_bytes, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* OFD_INPAINT_H */

@@ -1,4 +1,4 @@
-"""Loader for the native forward-warp library (libofd_fw.so, C ABI in include/ofd_fw.h).
+"""Loader for the native library (libofd_fw.so; C ABI in include/ofd_fw.h and include/ofd_inpaint.h).
 
 The library is built in-tree by :func:`opticalflowfromdepth_amd.build.build_native`
 (hipcc --offload-arch=gfx950).  There is deliberately NO fallback: if the
@@ -24,7 +24,7 @@ ABI_VERSION = 1
 _lock = threading.Lock()
 _lib = None
 
-# (name, argtypes, restype) for every symbol declared in include/ofd_fw.h
+# (name, argtypes, restype) for every symbol declared in include/*.h
 _P = ctypes.c_void_p
 _I64 = ctypes.c_int64
 _SZ = ctypes.c_size_t
@@ -39,6 +39,8 @@ SIGNATURES = {
     "ofd_fw_forward_warping_f64": ([_P] * 7 + [_I64] * 4 + [_P, _SZ, _P], ctypes.c_int),
     "ofd_fw_forward_warp_flow_f32": ([_P] * 6 + [_I64] * 4 + [_P, _SZ, _P], ctypes.c_int),
     "ofd_fw_forward_warp_flow_f64flow": ([_P] * 6 + [_I64] * 4 + [_P, _SZ, _P], ctypes.c_int),
+    "ofd_inpaint_workspace_bytes": ([_I64, _I64, _I64], _SZ),
+    "ofd_inpaint_telea_f32": ([_P] * 4 + [_I64] * 4 + [ctypes.c_int, _P, _SZ, _P], ctypes.c_int),
 }
 
 

@@ -1,7 +1,8 @@
 """In-tree build of the native forward-warp library for gfx950.
 
 ``python -m opticalflowfromdepth_amd.build`` or ``build_native()`` compiles
-csrc/ofd_fw.hip with hipcc into ``_build/libofd_fw.so`` (C ABI, include/ofd_fw.h).
+csrc/ofd_fw.hip (forward warp) and csrc/ofd_inpaint.hip (hole-fill) with hipcc
+into ``_build/libofd_fw.so`` (C ABI, include/ofd_fw.h and include/ofd_inpaint.h).
 The .so is git-ignored but travels with the repo snapshot to the GPU box.
 """
 from __future__ import annotations
@@ -13,8 +14,8 @@ import sys
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(_HERE)
-SRC = os.path.join(_HERE, "csrc", "ofd_fw.hip")
-HDR = os.path.join(REPO, "include", "ofd_fw.h")
+SRCS = [os.path.join(_HERE, "csrc", f) for f in ("ofd_fw.hip", "ofd_inpaint.hip")]
+HDRS = [os.path.join(REPO, "include", f) for f in ("ofd_fw.h", "ofd_inpaint.h")]
 OUT_DIR = os.path.join(_HERE, "_build")
 OUT = os.path.join(OUT_DIR, "libofd_fw.so")
 ARCH = os.environ.get("OFD_OFFLOAD_ARCH", "gfx950")
@@ -31,7 +32,7 @@ def needs_build() -> bool:
     if not os.path.exists(OUT):
         return True
     t = os.path.getmtime(OUT)
-    return any(os.path.getmtime(p) > t for p in (SRC, HDR))
+    return any(os.path.getmtime(p) > t for p in SRCS + HDRS + [os.path.abspath(__file__)])
 
 
 def build_native(force: bool = False, verbose: bool = False) -> str:
@@ -39,8 +40,10 @@ def build_native(force: bool = False, verbose: bool = False) -> str:
         return OUT
     os.makedirs(OUT_DIR, exist_ok=True)
     tmp = OUT + f".tmp{os.getpid()}"
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-I", os.path.join(REPO, "include"), "-o", tmp, SRC]
+    # -ffp-contract=off: the hole-fill's float / double sequence must be the
+    # oracle's bit for bit (the warp has no contractible arithmetic)
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
+           "-Wall", "-I", os.path.join(REPO, "include"), "-o", tmp] + SRCS
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

@@ -8,6 +8,9 @@ meaning, same checks and messages, same outputs, for any batch size B.
 ``forward_warp_flow`` is the batched FW.forward path (alt_cuda/fw.py:19-59)
 with the coordinate arithmetic fused into the splat kernel.
 
+``inpaint`` is the batched hole-fill that replaces ``utils.inpaint``
+(utils.py:136-151) with the layered Telea kernels of csrc/ofd_inpaint.hip.
+
 Both launch asynchronously on the current HIP stream of the input's device.
 There is no CPU path: the reference raises for non-GPU tensors
 (fw_cuda.cpp:11) and so does this module.
@@ -27,6 +30,8 @@ _F32, _F64 = torch.float32, torch.float64
 # workspace in the initial all-ones state (see include/ofd_fw.h).
 _ws_lock = threading.Lock()
 _workspaces: Dict[Tuple[int, int], torch.Tensor] = {}
+# hole-fill scratch, one per (device, stream); needs no initialisation
+_ip_workspaces: Dict[Tuple[int, int], torch.Tensor] = {}
 
 
 def _check_input(x: torch.Tensor, name: str) -> None:
@@ -147,3 +152,54 @@ def forward_warp_flow(obj: torch.Tensor, flow: torch.Tensor, depth: torch.Tensor
                 stream.cuda_stream)
         _native.check(rc, "forward_warp_flow")
     return output, valid, collision
+
+
+def inpaint(img: torch.Tensor, valid: torch.Tensor, collision: torch.Tensor, radius: int = 3) -> torch.Tensor:
+    """Drop-in for ``utils.inpaint(img, valid, collision)`` (utils.py:136-151), batched.
+
+    img [C,H,W] with valid / collision [1,H,W] (the reference's call shape), or
+    img [B,C,H,W] with [B,1,H,W] masks.  Pixels the keep mask of
+    utils.py:137-142 drops are filled (Telea weights, layered marching; see
+    include/ofd_inpaint.h); every pixel of the result is float32 of the
+    uint8 cast of utils.py:148, on img's device, like the reference's return.
+    """
+    for x, n in ((img, "img"), (valid, "valid"), (collision, "collision")):
+        if not isinstance(x, torch.Tensor):
+            raise TypeError(f"{n} must be a torch.Tensor")
+        if not x.is_cuda:
+            raise RuntimeError(f"{n} must be a CUDA tensor")
+    squeeze = img.dim() == 3
+    if squeeze:
+        img, valid, collision = img.unsqueeze(0), valid.unsqueeze(0), collision.unsqueeze(0)
+    if img.dim() != 4:
+        raise RuntimeError(f"img must be [C,H,W] or [B,C,H,W], got {img.dim()}-D")
+    B, C, H, W = img.shape
+    for x, n in ((valid, "valid"), (collision, "collision")):
+        if tuple(x.shape) != (B, 1, H, W):
+            raise RuntimeError(f"{n} must have shape {(B, 1, H, W)[1 if squeeze else 0:]}, "
+                               f"got {tuple(x.shape)[1 if squeeze else 0:]}")
+        if x.device != img.device:
+            raise RuntimeError(f"{n} is on {x.device}, img on {img.device}")
+    dev = img.device
+    with torch.cuda.device(dev):
+        stream = torch.cuda.current_stream(dev)
+        img = img.to(_F32).contiguous()
+        valid = valid.to(_F32).contiguous()
+        collision = collision.to(_F32).contiguous()
+        out = torch.empty_like(img)
+        lib = _native.lib()
+        nbytes = int(lib.ofd_inpaint_workspace_bytes(B, H, W))
+        ws = None
+        if nbytes:
+            key = (dev.index, stream.cuda_stream)
+            with _ws_lock:
+                ws = _ip_workspaces.get(key)
+                if ws is None or ws.numel() < nbytes:
+                    ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+                    _ip_workspaces[key] = ws
+        rc = lib.ofd_inpaint_telea_f32(img.data_ptr(), valid.data_ptr(), collision.data_ptr(), out.data_ptr(),
+                                       B, C, H, W, int(radius),
+                                       ws.data_ptr() if ws is not None else None,
+                                       ws.numel() if ws is not None else 0, stream.cuda_stream)
+        _native.check(rc, "inpaint")
+    return out[0] if squeeze else out

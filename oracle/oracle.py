@@ -36,8 +36,9 @@ _lib = None
 
 def build(force: bool = False) -> str:
     """Compile fw_oracle.c with gcc (oracle/Makefile)."""
-    if force or not os.path.exists(_LIB_PATH) or (
-        os.path.getmtime(_LIB_PATH) < os.path.getmtime(os.path.join(_HERE, "fw_oracle.c"))
+    srcs = [os.path.join(_HERE, f) for f in ("fw_oracle.c", "inpaint_oracle.c", "Makefile")]
+    if force or not os.path.exists(_LIB_PATH) or any(
+        os.path.getmtime(_LIB_PATH) < os.path.getmtime(f) for f in srcs
     ):
         subprocess.run(["make", "-s", "-C", _HERE], check=True)
     return _LIB_PATH
@@ -55,6 +56,10 @@ def _load():
             fn = getattr(lib, name)
             fn.restype = ctypes.c_int
             fn.argtypes = [fp] * nptr + [L, L, L, L, ctypes.c_int]
+        lib.oracle_inpaint_f32.restype = ctypes.c_int
+        lib.oracle_inpaint_f32.argtypes = [fp] * 4 + [L] * 4 + [ctypes.c_int] * 3
+        lib.oracle_inpaint_mask.restype = ctypes.c_int
+        lib.oracle_inpaint_mask.argtypes = [fp] * 3 + [L] * 3
         _lib = lib
     return _lib
 
@@ -186,3 +191,37 @@ def forward_warping_lexmin(obj, safe_y, safe_x, depth):
         valid[b, 0] = v.reshape(H, W)
         coll[b, 0] = (v & ~has).reshape(H, W)
     return out, valid, coll
+
+
+def inpaint(img, valid, collision, radius: int = 3, layered: bool = False, nthreads: int = 0):
+    """Restates a batched ``utils.inpaint`` (utils.py:136-151).
+
+    img [B,C,H,W], valid / collision [B,1,H,W] (cast to float32).  layered =
+    False: the sequential restatement of cv2.inpaint(..., INPAINT_TELEA)
+    (parity unpinned: OpenCV is absent); True: the layered Telea the GPU runs.
+    Returns float32 [B,C,H,W] holding uint8 values.
+    """
+    img = np.ascontiguousarray(img, dtype=np.float32)
+    valid = np.ascontiguousarray(valid, dtype=np.float32)
+    collision = np.ascontiguousarray(collision, dtype=np.float32)
+    B, C, H, W = img.shape
+    if valid.shape != (B, 1, H, W) or collision.shape != (B, 1, H, W):
+        raise ValueError("oracle.inpaint: shape mismatch")
+    out = np.empty_like(img)
+    rc = _load().oracle_inpaint_f32(_p(img), _p(valid), _p(collision), _p(out), B, C, H, W,
+                                    int(radius), int(bool(layered)), nthreads)
+    if rc != 0:
+        raise ValueError(f"oracle.inpaint rc={rc} (images must be at least 2x2)")
+    return out
+
+
+def inpaint_mask(valid, collision):
+    """utils.py:137-142: uint8 [B,H,W], 1 where cv2.inpaint fills."""
+    valid = np.ascontiguousarray(valid, dtype=np.float32)
+    collision = np.ascontiguousarray(collision, dtype=np.float32)
+    B, _, H, W = valid.shape
+    hole = np.empty((B, H, W), np.uint8)
+    rc = _load().oracle_inpaint_mask(_p(valid), _p(collision), _p(hole), B, H, W)
+    if rc != 0:
+        raise RuntimeError(f"oracle rc={rc}")
+    return hole

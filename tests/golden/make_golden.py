@@ -25,6 +25,13 @@ What it does, and what each fixture pins:
   :463) and ``geometry.py`` (imported as is): disparity and ego-motion flows
   with fixed seeds, and FW outputs on them.  Pins
   opticalflowfromdepth_amd.synth (flows within 1e-5) and realistic FW cases.
+* ``inpaint_mask.npz`` -- the reference's own ``utils.inpaint`` (utils.py:136-151,
+  taken by AST) run with a stand-in ``cv2`` namespace: ``dilate`` is a 3x3
+  in-image maximum (what cv2.dilate with a ones(3,3) kernel computes) and
+  ``inpaint`` records the uint8 image and mask it is handed and returns the
+  image unchanged.  Pins the keep-mask algebra (:137-142), the HWC uint8 cast
+  (:148) and the float32 return (:149-151) with the reference's own code; the
+  Telea fill values themselves stay unpinned (OpenCV is absent).
 
 Nothing from /root/reference is copied into the repo: only numeric arrays.
 """
@@ -89,6 +96,46 @@ def load_reference_utils_subset():
     mod.__dict__.update(torch=torch, np=np, random=random, math=math)
     exec(compile(ast.Module(body=body, type_ignores=[]), os.path.join(REF, "utils.py"), "exec"), mod.__dict__)
     return mod
+
+
+class _Cv2Recorder:
+    """Stand-in cv2 namespace for utils.inpaint: dilate restated, inpaint recorded."""
+    INPAINT_TELEA = 1
+
+    def __init__(self):
+        self.calls = []
+
+    @staticmethod
+    def dilate(M, kernel, iterations=1):
+        assert kernel.shape == (3, 3) and kernel.all() and iterations == 1
+        H, W = M.shape
+        pad = np.zeros((H + 2, W + 2), M.dtype)  # uint8 >= 0: a 0 border never wins the max
+        pad[1:-1, 1:-1] = M
+        return np.max(np.stack([pad[dy:dy + H, dx:dx + W] for dy in range(3) for dx in range(3)]), axis=0)
+
+    def inpaint(self, img, mask, radius, flags):
+        self.calls.append((img.copy(), mask.copy(), radius, flags))
+        return img.copy()
+
+
+class _CpuImage(torch.Tensor):
+    """utils.py:150 moves the result to img.get_device(), which is -1 for a CPU
+    tensor; this subclass names the CPU instead (the fixture runs on CPU)."""
+
+    def get_device(self):
+        return "cpu"
+
+
+def load_reference_inpaint():
+    """utils.inpaint taken by AST with the recorder as cv2."""
+    src = open(os.path.join(REF, "utils.py")).read()
+    tree = ast.parse(src)
+    body = [n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name == "inpaint"]
+    rec = _Cv2Recorder()
+    mod = types.ModuleType("utils_inpaint")
+    mod.__dict__.update(torch=torch, np=np, cv2=rec)
+    exec(compile(ast.Module(body=body, type_ignores=[]), os.path.join(REF, "utils.py"), "exec"), mod.__dict__)
+    return mod.inpaint, rec
 
 
 def load_reference_plausible_convert(utils_mod, geometry_mod):
@@ -239,6 +286,36 @@ def make_pipeline_cases(ref_fw, Plausible, Convert, utils_mod):
     return cases
 
 
+def make_inpaint_mask_cases(ref_inpaint, rec):
+    """utils.inpaint's mask algebra and casts on FW outputs and on masks with collisions."""
+    pl = np.load(os.path.join(HERE, "pipeline.npz"))
+    rng = np.random.default_rng(99)
+    inputs = []
+    for k in range(2):  # realistic: the warped RGB and masks of pipeline.npz
+        for tag in ("fw01", "fw03"):
+            o = pl[f"img{k}/{tag}_output"]
+            v, c = pl[f"img{k}/{tag}_valid"], pl[f"img{k}/{tag}_collision"]
+            inputs.append((o[0:3] * v, v, c))
+    for h, w in ((17, 23), (32, 40)):  # synthetic: collisions, isolated pixels, non-integer values
+        v = (rng.random((1, h, w)) < 0.7).astype(np.float32)
+        c = ((rng.random((1, h, w)) < 0.3) & (v > 0)).astype(np.float32)
+        img = (rng.uniform(-20, 300, (3, h, w))).astype(np.float32)
+        inputs.append((img, v, c))
+    cases = {}
+    for n, (img, v, c) in enumerate(inputs):
+        rec.calls.clear()
+        got = ref_inpaint(torch.from_numpy(np.ascontiguousarray(img)).as_subclass(_CpuImage),
+                          torch.from_numpy(v), torch.from_numpy(c))
+        got = got.as_subclass(torch.Tensor)
+        (img_u8, mask, radius, flags), = rec.calls
+        assert radius == 3 and flags == _Cv2Recorder.INPAINT_TELEA
+        assert got.dtype == torch.float32 and tuple(got.shape) == img.shape
+        cases.update({f"c{n}/img": img, f"c{n}/valid": v, f"c{n}/collision": c,
+                      f"c{n}/img_u8_hwc": img_u8, f"c{n}/mask": mask, f"c{n}/returned": got.numpy()})
+    cases["n"] = np.array(len(inputs))
+    return cases
+
+
 def main():
     ref_fw = load_reference_fw()
     geometry_mod = load_reference_geometry()
@@ -251,7 +328,10 @@ def main():
     np.savez_compressed(os.path.join(HERE, "fw_wrapper.npz"), **wr)
     pl = make_pipeline_cases(ref_fw, Plausible, Convert, utils_mod)
     np.savez_compressed(os.path.join(HERE, "pipeline.npz"), **pl)
-    for f in ("fw_op.npz", "fw_wrapper.npz", "pipeline.npz"):
+    ref_inpaint, rec = load_reference_inpaint()
+    im = make_inpaint_mask_cases(ref_inpaint, rec)
+    np.savez_compressed(os.path.join(HERE, "inpaint_mask.npz"), **im)
+    for f in ("fw_op.npz", "fw_wrapper.npz", "pipeline.npz", "inpaint_mask.npz"):
         print(f, os.path.getsize(os.path.join(HERE, f)), "bytes")
 
 

@@ -10,8 +10,11 @@ from conftest import REPO
 
 
 def _header_symbols():
-    txt = open(os.path.join(REPO, "include", "ofd_fw.h")).read()
-    return sorted(set(re.findall(r"\b(ofd_fw_\w+)\s*\(", txt)))
+    syms = set()
+    for h in ("ofd_fw.h", "ofd_inpaint.h"):
+        txt = open(os.path.join(REPO, "include", h)).read()
+        syms |= set(re.findall(r"\b(ofd_(?:fw|inpaint)_\w+)\s*\(", txt))
+    return sorted(syms)
 
 
 def test_library_exports_every_header_symbol():
@@ -76,6 +79,21 @@ def test_argument_errors_without_gpu():
     assert lib.ofd_fw_forward_warp_flow_f32(*([None] * 6), 1, 6, 4, 4, None, 0, None) == -1
 
 
+def test_inpaint_argument_errors_without_gpu():
+    from opticalflowfromdepth_amd import _native
+    lib = _native.lib()
+    f = lib.ofd_inpaint_telea_f32
+    assert f(*([None] * 4), 0, 3, 8, 8, 3, None, 0, None) == 0        # empty batch: no-op
+    assert f(*([None] * 4), 1, 3, 8, 8, 3, None, 0, None) == -1       # null pointers
+    p = ctypes.c_void_p(16)                                            # never dereferenced
+    assert f(p, p, p, p, 1, 3, 1, 8, 3, None, 0, None) == -1          # H < 2
+    assert f(p, p, p, p, 1, 3, 4096, 4097, 3, None, 0, None) == -2   # H + W > 8192
+    assert f(p, p, p, p, 1, 3, 8, 8, 3, None, 0, None) == -3          # no workspace
+    one = lib.ofd_inpaint_workspace_bytes(1, 768, 1024)
+    assert one >= 768 * 1024 * 14
+    assert lib.ofd_inpaint_workspace_bytes(4, 768, 1024) >= 4 * (one - 256)
+
+
 def test_ops_reject_cpu_tensors_like_reference():
     import fw_cuda
     from opticalflowfromdepth_amd import FW
@@ -117,6 +135,8 @@ def test_c_abi_header_compiles_as_c():
     import tempfile
     with tempfile.TemporaryDirectory() as d:
         c = os.path.join(d, "t.c")
-        open(c, "w").write('#include "ofd_fw.h"\nint main(void){int (*f)(void) = ofd_fw_abi_version; (void)f; return OFD_FW_OK;}\n')
+        open(c, "w").write('#include "ofd_fw.h"\n#include "ofd_inpaint.h"\nint main(void){int (*f)(void) = '
+                           'ofd_fw_abi_version; size_t (*g)(int64_t, int64_t, int64_t) = ofd_inpaint_workspace_bytes; '
+                           '(void)f; (void)g; return OFD_FW_OK;}\n')
         subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-c", "-I", os.path.join(REPO, "include"),
                         c, "-o", os.path.join(d, "t.o")], check=True)
