@@ -18,7 +18,7 @@
 // results do not depend on the order of its pixels.  The CPU restatement is
 // oracle/inpaint_oracle.c (layered mode); cv2 parity is unpinned (no OpenCV).
 //
-// Four launches per chunk of images:
+// Launches per chunk of images:
 //   PREP   one thread per pixel: keep mask (3x3 dilation of valid != coll),
 //          hole bits, out = float(uint8(img)) for every pixel.
 //   COLS   one thread per column: vertical distances to the nearest known /
@@ -26,9 +26,10 @@
 //   ROWS   one thread per row: the row pass of both L1 distance transforms,
 //          the Chebyshev-radius test of the outer band; writes the per-pixel
 //          code (hole layer / band / ring layer / far) and initial T.
-//   TELEA  one 1024-thread workgroup per image: counting sort of the pixels by
-//          layer (LDS histogram + block scan), then the outer-band layers and
-//          the hole layers, one workgroup barrier per layer.
+//   SORT   chip-wide counting sort of ring pixels and holes by layer (LDS
+//          histograms, one scan, one host read of the layer counts).
+//   LAYERS one launch per outer-band layer and per hole layer, one thread
+//          per pixel of every image of the chunk.
 //
 // Plain HIP for gfx950; FP contraction off so the float / double sequence is
 // the oracle's.
@@ -53,7 +54,6 @@ constexpr int DINF = 0x3FFF;  // distance "infinity" in the transforms (> H + W)
 constexpr int kMaxHW = 8192;  // H + W limit: layers fit 13 bits, bins fit LDS
 constexpr int kMaxRange = 100;
 constexpr int kMaxBins = kMaxHW + 2 * kMaxRange;
-constexpr int kTeleaThreads = 1024;
 constexpr int kChanGroup = 4;  // channels accumulated together per window pass
 
 inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
@@ -335,13 +335,204 @@ __device__ void telea_colour(const Img &m, int y, int x, unsigned L, float tij, 
     }
 }
 
-// exclusive block scan of bins[0, n) in place (1024 threads)
-__device__ void block_exclusive_scan(unsigned *bins, int n, unsigned *wsum) {
+// telea_colour for range 3 (the reference's inpaintRange) with register
+// patches: the 9x9 patches of INSIDE flags, distances and channel values
+// around the hole are loaded once (every load independent of the others),
+// then weights and sums are formed in telea_colour's exact (k, l) order, so
+// the result is bit-identical.
+//   kBorder = false: window plus one-pixel halo inside the image, no border
+//     index shifts; every sampled position is then a finalised pixel, so
+//     values come straight from `out`.
+//   kBorder = true: any position; out-of-image patch entries read as KNOWN
+//     with t = 1e6 (cv2's padded border), cv2's km / kp / lm / lp shifts at
+//     the image border become selects between neighbouring patch entries, and
+//     a sampled pixel still INSIDE reads as its input value (sample()).
+constexpr bool in_disk3(int a, int b) { return a * a + b * b <= 9; }
+constexpr bool need3(int a, int b) {  // in the disk, or a 4-neighbour of a disk position
+    return in_disk3(a, b) || in_disk3(a - 1, b) || in_disk3(a + 1, b) || in_disk3(a, b - 1) || in_disk3(a, b + 1);
+}
+constexpr int pidx(int a, int b) { return (a + 4) * 9 + (b + 4); }
+
+template <bool kBorder>
+__device__ __forceinline__ void telea_pixel_r3(const Img &m, int y, int x, unsigned L, int64_t p) {
+    const int W = m.W, H = m.H;
+    // patch position (a, b) -> in-image flag and (clamped) pixel index; every
+    // load below is unconditional, so they all issue before the first use
+    auto inimg = [&](int a, int b) -> bool {
+        return !kBorder || (y + a >= 0 && y + a < H && x + b >= 0 && x + b < W);
+    };
+    auto at = [&](int a, int b) -> int64_t {
+        if (!kBorder) return p + int64_t(a) * W + b;
+        const int yy = min(max(y + a, 0), H - 1), xx = min(max(x + b, 0), W - 1);
+        return int64_t(yy) * W + xx;
+    };
+    unsigned cds[81];
+#pragma unroll
+    for (int a = -4; a <= 4; ++a)
+#pragma unroll
+        for (int b = -4; b <= 4; ++b)
+            if (need3(a, b)) cds[pidx(a, b)] = m.code[at(a, b)];
+    float tk[81];
+#pragma unroll
+    for (int a = -3; a <= 3; ++a)
+#pragma unroll
+        for (int b = -3; b <= 3; ++b)
+            if (in_disk3(a, b) && (a || b)) tk[pidx(a, b)] = m.T[at(a, b)];
+    uint32_t ib[3] = {0u, 0u, 0u};  // INSIDE bit per patch position (0 outside the image)
+#pragma unroll
+    for (int a = -4; a <= 4; ++a)
+#pragma unroll
+        for (int b = -4; b <= 4; ++b) {
+            if (!need3(a, b)) continue;
+            const unsigned cd = cds[pidx(a, b)];
+            const unsigned in = (inimg(a, b) && (cd & C_HOLE) && (cd & LAY) >= L) ? 1u : 0u;
+            ib[pidx(a, b) >> 5] |= in << (pidx(a, b) & 31);
+        }
+    auto IN = [&](int a, int b) -> bool { return (ib[pidx(a, b) >> 5] >> (pidx(a, b) & 31)) & 1u; };
+    // distances as tval() reads them: INSIDE or outside the image -> 1e6
+#pragma unroll
+    for (int a = -3; a <= 3; ++a)
+#pragma unroll
+        for (int b = -3; b <= 3; ++b)
+            if (in_disk3(a, b) && (a || b)) tk[pidx(a, b)] = (IN(a, b) || !inimg(a, b)) ? T_FAR : tk[pidx(a, b)];
+    // fm_dist<false>
+    const float tij = min4f(fm_solve(tk[pidx(-1, 0)], IN(-1, 0), tk[pidx(0, -1)], IN(0, -1)),
+                            fm_solve(tk[pidx(1, 0)], IN(1, 0), tk[pidx(0, -1)], IN(0, -1)),
+                            fm_solve(tk[pidx(-1, 0)], IN(-1, 0), tk[pidx(0, 1)], IN(0, 1)),
+                            fm_solve(tk[pidx(1, 0)], IN(1, 0), tk[pidx(0, 1)], IN(0, 1)));
+    m.T[p] = tij;
+    float gtx, gty;
+    if (!IN(0, 1))
+        gtx = !IN(0, -1) ? (tk[pidx(0, 1)] - tk[pidx(0, -1)]) * 0.5f : (tk[pidx(0, 1)] - tij);
+    else
+        gtx = !IN(0, -1) ? (tij - tk[pidx(0, -1)]) : 0.f;
+    if (!IN(1, 0))
+        gty = !IN(-1, 0) ? (tk[pidx(1, 0)] - tk[pidx(-1, 0)]) * 0.5f : (tk[pidx(1, 0)] - tij);
+    else
+        gty = !IN(-1, 0) ? (tij - tk[pidx(-1, 0)]) : 0.f;
+    auto used = [&](int a, int b) -> bool { return in_disk3(a, b) && (a || b) && inimg(a, b) && !IN(a, b); };
+    float wt[81];
+    float s = 1.0e-20f;
+#pragma unroll
+    for (int a = -3; a <= 3; ++a)
+#pragma unroll
+        for (int b = -3; b <= 3; ++b) {
+            if (!in_disk3(a, b) || !(a || b)) continue;
+            const float ry = float(-a), rx = float(-b);
+            const float len2 = rx * rx + ry * ry;
+            const float dst = float(1. / (double(len2) * sqrt(double(len2))));
+            const float lev = float(1. / (1 + fabs(double(tk[pidx(a, b)] - tij))));
+            float dir = rx * gtx + ry * gty;
+            if (fabs(double(dir)) <= 0.01) dir = 0.000001f;
+            const float w = float(fabs(double(dst * lev * dir)));
+            wt[pidx(a, b)] = used(a, b) ? w : 0.f;
+            s = used(a, b) ? s + w : s;
+        }
+    for (int c = 0; c < m.C; ++c) {
+        const float *ob = m.out + int64_t(c) * m.HW;
+        const float *ib0 = m.img + int64_t(c) * m.HW;
+        float V[81];
+#pragma unroll
+        for (int a = -4; a <= 4; ++a)
+#pragma unroll
+            for (int b = -4; b <= 4; ++b) {
+                if (kBorder) {
+                    const float vo = ob[at(a, b)], vi = float(to_u8(ib0[at(a, b)]));
+                    V[pidx(a, b)] = IN(a, b) ? vi : vo;  // outside the image: never sampled
+                } else if (need3(a, b) && (a || b)) {
+                    V[pidx(a, b)] = ob[at(a, b)];
+                }
+            }
+        float Ia = 0.f, Jx = 0.f, Jy = 0.f;
+#pragma unroll
+        for (int a = -3; a <= 3; ++a)
+#pragma unroll
+            for (int b = -3; b <= 3; ++b) {
+                if (!in_disk3(a, b) || !(a || b)) continue;
+                const float ry = float(-a), rx = float(-b), w = wt[pidx(a, b)];
+                const bool nr = !IN(a, b + 1), nl = !IN(a, b - 1), nd = !IN(a + 1, b), nu = !IN(a - 1, b);
+                float sc, gix, giy;
+                if (!kBorder) {
+                    sc = V[pidx(a, b)];
+                    gix = nr ? (nl ? (V[pidx(a, b + 1)] - V[pidx(a, b - 1)]) * 2.0f : (V[pidx(a, b + 1)] - sc))
+                             : (nl ? (sc - V[pidx(a, b - 1)]) : 0.f);
+                    giy = nd ? (nu ? (V[pidx(a + 1, b)] - V[pidx(a - 1, b)]) * 2.0f : (V[pidx(a + 1, b)] - sc))
+                             : (nu ? (sc - V[pidx(a - 1, b)]) : 0.f);
+                } else {
+                    // cv2's shifted rows / columns: km = k + (k == 0), kp = k - (k == H-1),
+                    // lm = l + (l == 0), lp = l - (l == W-1) (telea_colour)
+                    const bool t0 = y + a == 0, tH = y + a == H - 1, l0 = x + b == 0, lW = x + b == W - 1;
+                    auto Vs = [&](int r0, bool rs, int c0, bool cs) -> float {  // V(r0 + rs, c0 + cs)
+                        const float v00 = V[pidx(r0, c0)], v01 = V[pidx(r0, c0 + 1)];
+                        const float v10 = V[pidx(r0 + 1, c0)], v11 = V[pidx(r0 + 1, c0 + 1)];
+                        return rs ? (cs ? v11 : v10) : (cs ? v01 : v00);
+                    };
+                    // rows: km in {a, a+1}, km-1 in {a-1, a}, kp in {a-1, a}, kp+1 in {a, a+1}
+                    // cols: lm in {b, b+1}, lm-1 in {b-1, b}, lp in {b-1, b}, lp+1 in {b, b+1}
+                    sc = Vs(a, t0, b, l0);                     // (km, lm)
+                    const float v_km_lp1 = Vs(a, t0, b, !lW);  // (km, lp+1)
+                    const float v_km_lmm = Vs(a, t0, b - 1, l0);
+                    const float v_km_lp = Vs(a, t0, b - 1, !lW);
+                    const float v_kp1_lm = Vs(a, !tH, b, l0);
+                    const float v_kmm_lm = Vs(a - 1, t0, b, l0);
+                    const float v_kp_lm = Vs(a - 1, !tH, b, l0);
+                    gix = nr ? (nl ? (v_km_lp1 - v_km_lmm) * 2.0f : (v_km_lp1 - sc)) : (nl ? (v_km_lp - v_km_lmm) : 0.f);
+                    giy = nd ? (nu ? (v_kp1_lm - v_kmm_lm) * 2.0f : (v_kp1_lm - sc)) : (nu ? (v_kp_lm - v_kmm_lm) : 0.f);
+                }
+                // unused positions have w == 0: adding +-0 never changes a sum of finite terms
+                // except the sign of an exact zero, which the final expression cannot see
+                if (used(a, b)) {
+                    Ia += w * sc;
+                    Jx -= w * (gix * rx);
+                    Jy -= w * (giy * ry);
+                }
+            }
+        const float sat =
+            float(double(Ia / s) + double(Jx + Jy) / (sqrt(double(Jx * Jx + Jy * Jy)) + double(1.0e-20f)) + double(0.5f));
+        m.out[int64_t(c) * m.HW + p] = float(sat_u8(sat));
+    }
+}
+
+// ---------------------------------------------------------------- SORT
+// Counting sort of the chunk's ring pixels and holes by layer, chip-wide:
+// bins 0 .. nring-1 = ring layers 1 .., bins nring .. = hole layers 1 ..; an
+// entry is bl * HW + p (chunk-local image bl, pixel p).  HIST and SCATTER
+// aggregate per workgroup in LDS, so the global atomics are one per
+// (workgroup, nonempty bin).  Order inside a bin is irrelevant.
+constexpr int kSortThreads = 256;
+constexpr int kSortSpan = 16384;  // pixels per sort workgroup
+
+__device__ __forceinline__ int bin_of(unsigned cd, int nring) {
+    const unsigned l = cd & LAY;
+    if (cd & C_HOLE) return l != LAY_INF ? nring + int(l) - 1 : -1;
+    if (cd & C_RING) return int(l) - 1;
+    return -1;
+}
+
+__global__ __launch_bounds__(kSortThreads) void ip_hist_kernel(const uint16_t *__restrict__ code,
+                                                               unsigned *__restrict__ hist, int64_t total, int nring) {
+    __shared__ unsigned h[kMaxBins];
+    for (int k = threadIdx.x; k < kMaxBins; k += kSortThreads) h[k] = 0;
+    __syncthreads();
+    const int64_t beg = int64_t(blockIdx.x) * kSortSpan, end = min(beg + kSortSpan, total);
+    for (int64_t e = beg + threadIdx.x; e < end; e += kSortThreads) {
+        const int bin = bin_of(code[e], nring);
+        if (bin >= 0) atomicAdd(&h[bin], 1u);
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < kMaxBins; k += kSortThreads)
+        if (h[k]) atomicAdd(&hist[k], h[k]);
+}
+
+// cursor[k] = exclusive prefix sum of hist (one workgroup)
+__global__ __launch_bounds__(1024) void ip_scan_kernel(const unsigned *__restrict__ hist, unsigned *__restrict__ cursor,
+                                                       int n) {
+    __shared__ unsigned wsum[16];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int per = (n + kTeleaThreads - 1) / kTeleaThreads;
+    const int per = (n + 1023) / 1024;
     const int beg = min(tid * per, n), end = min(beg + per, n);
     unsigned sum = 0;
-    for (int i = beg; i < end; ++i) sum += bins[i];
+    for (int i = beg; i < end; ++i) sum += hist[i];
     unsigned incl = sum;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -352,7 +543,7 @@ __device__ void block_exclusive_scan(unsigned *bins, int n, unsigned *wsum) {
     __syncthreads();
     if (tid == 0) {
         unsigned acc = 0;
-        for (int k = 0; k < kTeleaThreads / 64; ++k) {
+        for (int k = 0; k < 16; ++k) {
             const unsigned v = wsum[k];
             wsum[k] = acc;
             acc += v;
@@ -361,98 +552,105 @@ __device__ void block_exclusive_scan(unsigned *bins, int n, unsigned *wsum) {
     __syncthreads();
     unsigned excl = incl - sum + wsum[wave];
     for (int i = beg; i < end; ++i) {
-        const unsigned v = bins[i];
-        bins[i] = excl;
-        excl += v;
+        cursor[i] = excl;
+        excl += hist[i];
     }
-    __syncthreads();
 }
 
-__global__ __launch_bounds__(kTeleaThreads) void ip_telea_kernel(const float *__restrict__ img, float *__restrict__ out,
-                                                                 IpWs ws, int C, int H, int W, int range, int64_t b0) {
-    __shared__ unsigned bins[kMaxBins];
-    __shared__ unsigned wsum[kTeleaThreads / 64];
-    __shared__ unsigned maxin;
-    const int tid = threadIdx.x;
-    const int64_t HW = int64_t(H) * W, bl = blockIdx.x, b = b0 + bl;
-    Img m;
-    m.code = ws.code + bl * HW;
-    m.T = ws.T + bl * HW;
-    m.img = img + b * int64_t(C) * HW;
-    m.out = out + b * int64_t(C) * HW;
-    m.H = H;
-    m.W = W;
-    m.C = C;
-    m.HW = HW;
-    uint32_t *list = ws.list + bl * HW;
-    const int nring = 2 * range;  // ring layers are 1 .. 2r - 1
-    // ---- counting sort of ring pixels (bins 0 .. nring-1) and holes (bins nring ..) by layer
-    for (int k = tid; k < kMaxBins; k += kTeleaThreads) bins[k] = 0;
-    if (tid == 0) maxin = 0;
+__global__ __launch_bounds__(kSortThreads) void ip_scatter_kernel(const uint16_t *__restrict__ code,
+                                                                  unsigned *__restrict__ cursor,
+                                                                  uint32_t *__restrict__ list, int64_t total,
+                                                                  int nring) {
+    __shared__ unsigned h[kMaxBins];
+    for (int k = threadIdx.x; k < kMaxBins; k += kSortThreads) h[k] = 0;
     __syncthreads();
-    for (int64_t p = tid; p < HW; p += kTeleaThreads) {
-        const unsigned cd = m.code[p], l = cd & LAY;
-        if (cd & C_HOLE) {
-            if (l != LAY_INF) {
-                atomicAdd(&bins[nring + int(l) - 1], 1u);
-                atomicMax(&maxin, l);
-            }
-        } else if (cd & C_RING) {
-            atomicAdd(&bins[int(l) - 1], 1u);
-        }
+    const int64_t beg = int64_t(blockIdx.x) * kSortSpan, end = min(beg + kSortSpan, total);
+    for (int64_t e = beg + threadIdx.x; e < end; e += kSortThreads) {
+        const int bin = bin_of(code[e], nring);
+        if (bin >= 0) atomicAdd(&h[bin], 1u);
     }
     __syncthreads();
-    const int nbins = nring + int(maxin);
-    block_exclusive_scan(bins, nbins, wsum);
-    for (int64_t p = tid; p < HW; p += kTeleaThreads) {
-        const unsigned cd = m.code[p], l = cd & LAY;
-        int bin = -1;
-        if (cd & C_HOLE) {
-            if (l != LAY_INF) bin = nring + int(l) - 1;
-        } else if (cd & C_RING) {
-            bin = int(l) - 1;
-        }
-        if (bin >= 0) list[atomicAdd(&bins[bin], 1u)] = uint32_t(p);
-    }
+    for (int k = threadIdx.x; k < kMaxBins; k += kSortThreads)
+        if (h[k]) h[k] = atomicAdd(&cursor[k], h[k]);  // this workgroup's range of bin k
     __syncthreads();
-    // bin k now spans [k ? bins[k-1] : 0, bins[k])
-    // ---- outer band: icvCalcFMM over the ring, layer by layer, then negated
-    for (int L = 1; L < nring; ++L) {
-        const unsigned beg = L > 1 ? bins[L - 2] : 0u, end = bins[L - 1];
-        for (unsigned i = beg + tid; i < end; i += kTeleaThreads) {
-            const uint32_t p = list[i];
-            const int y = int(p / unsigned(W)), x = int(p - unsigned(y) * unsigned(W));
-            m.T[p] = fm_dist<true>(m, y, x, unsigned(L));
-        }
-        __syncthreads();
-    }
-    {
-        const unsigned end = bins[nring - 1];
-        for (unsigned i = tid; i < end; i += kTeleaThreads) {
-            const uint32_t p = list[i];
-            m.T[p] = -m.T[p];
-        }
-    }
-    __syncthreads();
-    // ---- holes, layer by layer
-    for (int L = 1; L <= int(maxin); ++L) {
-        const int k = nring + L - 1;
-        const unsigned beg = bins[k - 1], end = bins[k];
-        for (unsigned i = beg + tid; i < end; i += kTeleaThreads) {
-            const uint32_t p = list[i];
-            const int y = int(p / unsigned(W)), x = int(p - unsigned(y) * unsigned(W));
-            const float t = fm_dist<false>(m, y, x, unsigned(L));
-            m.T[p] = t;
-            for (int c0 = 0; c0 < C; c0 += kChanGroup) {
-                const int n = min(kChanGroup, C - c0);
-                unsigned res[kChanGroup];
-                telea_colour(m, y, x, unsigned(L), t, range, c0, n, res);
-                for (int c = 0; c < n; ++c) m.out[(c0 + c) * HW + p] = float(res[c]);
-            }
-        }
-        __syncthreads();
+    for (int64_t e = beg + threadIdx.x; e < end; e += kSortThreads) {
+        const int bin = bin_of(code[e], nring);
+        if (bin >= 0) list[atomicAdd(&h[bin], 1u)] = uint32_t(e);
     }
 }
+
+// ---------------------------------------------------------------- LAYERS
+// One launch per layer over every image of the chunk, one thread per pixel.
+struct Chunk {
+    const uint16_t *code;
+    float *T;
+    const float *img;
+    float *out;
+    int C, H, W;
+    int64_t HW, b0;
+};
+
+__device__ __forceinline__ Img image_of(const Chunk &ch, uint32_t e, int &y, int &x, int64_t &p) {
+    const int64_t bl = int64_t(e) / ch.HW, b = ch.b0 + bl;
+    p = int64_t(e) - bl * ch.HW;
+    y = int(p / ch.W);
+    x = int(p - int64_t(y) * ch.W);
+    Img m;
+    m.code = ch.code + bl * ch.HW;
+    m.T = ch.T + bl * ch.HW;
+    m.img = ch.img + b * int64_t(ch.C) * ch.HW;
+    m.out = ch.out + b * int64_t(ch.C) * ch.HW;
+    m.H = ch.H;
+    m.W = ch.W;
+    m.C = ch.C;
+    m.HW = ch.HW;
+    return m;
+}
+
+// outer band (icvCalcFMM over the ring): ring layer L
+__global__ __launch_bounds__(256) void ip_ring_layer_kernel(Chunk ch, const uint32_t *__restrict__ list, unsigned n,
+                                                            unsigned L) {
+    const unsigned i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    int y, x;
+    int64_t p;
+    const Img m = image_of(ch, list[i], y, x, p);
+    m.T[p] = fm_dist<true>(m, y, x, L);
+}
+
+// the outer band's distances are negative (icvCalcFMM negate = true)
+__global__ __launch_bounds__(256) void ip_negate_kernel(float *__restrict__ T, const uint32_t *__restrict__ list,
+                                                        unsigned n) {
+    const unsigned i = blockIdx.x * 256u + threadIdx.x;
+    if (i < n) T[list[i]] = -T[list[i]];
+}
+
+// hole layer L: distance, then every channel's Telea colour
+__global__ __launch_bounds__(256) void ip_hole_layer_kernel(Chunk ch, const uint32_t *__restrict__ list, unsigned n,
+                                                            unsigned L, int range) {
+    const unsigned i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    int y, x;
+    int64_t p;
+    const Img m = image_of(ch, list[i], y, x, p);
+    if (range == 3) {
+        if (y >= 4 && y < m.H - 4 && x >= 4 && x < m.W - 4)
+            telea_pixel_r3<false>(m, y, x, L, p);
+        else
+            telea_pixel_r3<true>(m, y, x, L, p);
+        return;
+    }
+    const float t = fm_dist<false>(m, y, x, L);
+    m.T[p] = t;
+    for (int c0 = 0; c0 < m.C; c0 += kChanGroup) {
+        const int nc = min(kChanGroup, m.C - c0);
+        unsigned res[kChanGroup];
+        telea_colour(m, y, x, L, t, range, c0, nc, res);
+        for (int c = 0; c < nc; ++c) m.out[(c0 + c) * m.HW + p] = float(res[c]);
+    }
+}
+
+inline unsigned blocks_for(unsigned n, unsigned per) { return (n + per - 1) / per; }
 
 }  // namespace
 
@@ -460,7 +658,7 @@ extern "C" {
 
 size_t ofd_inpaint_workspace_bytes(int64_t B, int64_t H, int64_t W) {
     if (B <= 0 || H <= 0 || W <= 0) return 0;
-    return size_t(B) * per_image(H, W) + 256;
+    return size_t(B) * per_image(H, W) + 2 * align256(size_t(kMaxBins) * 4) + 256;
 }
 
 int ofd_inpaint_telea_f32(const float *img, const float *valid, const float *collision, float *out, int64_t B,
@@ -472,24 +670,61 @@ int ofd_inpaint_telea_f32(const float *img, const float *valid, const float *col
     if (H < 2 || W < 2) return OFD_FW_EINVAL;
     if (H + W > kMaxHW || H * W >= (int64_t(1) << 31)) return OFD_FW_ETOOBIG;
     const int r = radius < 1 ? 1 : (radius > kMaxRange ? kMaxRange : radius);
+    const int nring = 2 * r;  // ring layers 1 .. 2r-1 (a Chebyshev-r neighbour is <= 2r away in L1)
     const int64_t HW = H * W;
     const size_t pi = per_image(H, W);
+    const size_t fixed = 2 * align256(size_t(kMaxBins) * 4);
     if (!workspace || (reinterpret_cast<uintptr_t>(workspace) & 255u)) return OFD_FW_EWORKSPACE;
-    int64_t G = int64_t(workspace_bytes / pi);
-    if (G < 1) return OFD_FW_EWORKSPACE;
+    if (workspace_bytes < fixed + pi) return OFD_FW_EWORKSPACE;
+    int64_t G = int64_t((workspace_bytes - fixed) / pi);
+    const int64_t gcap = ((int64_t(1) << 31) - 1) / HW;  // list entries bl * HW + p fit 31 bits
+    if (G > gcap) G = gcap;
     if (G > B) G = B;
     hipStream_t st = static_cast<hipStream_t>(stream);
-    const IpWs w = carve(workspace, G, HW);
+    unsigned *hist = reinterpret_cast<unsigned *>(workspace);
+    unsigned *cursor = reinterpret_cast<unsigned *>(static_cast<char *>(workspace) + align256(size_t(kMaxBins) * 4));
+    const IpWs w = carve(static_cast<char *>(workspace) + fixed, G, HW);
+    const int nbins = nring + int(H + W);
+    unsigned hh[kMaxBins];
     for (int64_t b0 = 0; b0 < B; b0 += G) {
         const int64_t nb = B - b0 < G ? B - b0 : G;
+        const int64_t total = nb * HW;
         hipLaunchKernelGGL(ip_prep_kernel, dim3(unsigned((W + 63) / 64), unsigned((H + 3) / 4), unsigned(nb)),
                            dim3(256), 0, st, img, valid, collision, out, w.code, int(C), int(H), int(W), b0);
         hipLaunchKernelGGL(ip_cols_kernel, dim3(unsigned((W + 255) / 256), unsigned(nb)), dim3(256), 0, st, w.code,
                            w.gcol, int(H), int(W));
         hipLaunchKernelGGL(ip_rows_kernel, dim3(unsigned((H + 63) / 64), unsigned(nb)), dim3(64), 0, st, w.code, w.T,
                            w.gcol, w.list, int(H), int(W), r);
-        hipLaunchKernelGGL(ip_telea_kernel, dim3(unsigned(nb)), dim3(kTeleaThreads), 0, st, img, out, w, int(C),
-                           int(H), int(W), r, b0);
+        hipError_t e = hipMemsetAsync(hist, 0, size_t(kMaxBins) * 4, st);
+        if (e != hipSuccess) return int(e);
+        const unsigned sblocks = unsigned((total + kSortSpan - 1) / kSortSpan);
+        hipLaunchKernelGGL(ip_hist_kernel, dim3(sblocks), dim3(kSortThreads), 0, st, w.code, hist, total, nring);
+        hipLaunchKernelGGL(ip_scan_kernel, dim3(1), dim3(1024), 0, st, hist, cursor, nbins);
+        // the layer counts size the per-layer launches: one host round trip per chunk
+        e = hipMemcpyAsync(hh, hist, size_t(nbins) * 4, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) return int(e);
+        hipLaunchKernelGGL(ip_scatter_kernel, dim3(sblocks), dim3(kSortThreads), 0, st, w.code, cursor, w.list, total,
+                           nring);
+        const Chunk ch{w.code, w.T, img, out, int(C), int(H), int(W), HW, b0};
+        unsigned off = 0;
+        for (int L = 1; L < nring; ++L) {  // outer band, then negated
+            const unsigned n = hh[L - 1];
+            if (n)
+                hipLaunchKernelGGL(ip_ring_layer_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, st, ch, w.list + off,
+                                   n, unsigned(L));
+            off += n;
+        }
+        off += hh[nring - 1];  // always empty (ring layers stop at 2r - 1)
+        if (off)
+            hipLaunchKernelGGL(ip_negate_kernel, dim3(blocks_for(off, 256)), dim3(256), 0, st, w.T, w.list, off);
+        for (int L = 1; nring + L - 1 < nbins; ++L) {  // holes
+            const unsigned n = hh[nring + L - 1];
+            if (n)
+                hipLaunchKernelGGL(ip_hole_layer_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, st, ch, w.list + off,
+                                   n, unsigned(L), r);
+            off += n;
+        }
     }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? OFD_FW_OK : int(e);
