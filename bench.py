@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
     ap.add_argument("--check", action="store_true", help="verify one image against the oracle")
     ap.add_argument("--engine", choices=["tile", "split", "atomic"], default="tile")
+    ap.add_argument("--no-hole-fill", action="store_true", help="skip the config-3 hole-fill phase")
+    ap.add_argument("--hole-fill-steps", type=int, default=5)
     return ap.parse_args()
 
 
@@ -62,8 +64,6 @@ def cpu_baseline(obj, flow, depth, budget_s, threads):
     o = obj[idx].cpu().numpy()
     f = flow[idx].cpu().numpy()
     d = depth[idx].cpu().numpy()
-    if threads <= 0:
-        threads = min(16, os.cpu_count() or 1)
     oracle.fw_flow(o[:1], f[:1], d[:1], nthreads=threads)  # warm (build + page-in)
     reps, t0 = 0, time.perf_counter()
     while True:
@@ -77,6 +77,57 @@ def cpu_baseline(obj, flow, depth, budget_s, threads):
             "sample": f"{n_img} images (of the {B}-image batch, both flow kinds) x {reps} reps, "
                       f"C={o.shape[1]}, {o.shape[2]}x{o.shape[3]}, oracle/fw_oracle.c serial-per-plane "
                       f"loop, {el:.1f} s wall on {platform.processor() or platform.machine()}"}
+
+
+def hole_fill_phase(out, valid, coll, steps, stream):
+    """BASELINE config 3's hole-fill, reported as its own phase:
+    utils.inpaint on the warped RGB of this batch (preprocess.py:362-366),
+    batched on the GPU.  28 algorithmic B/px (RGB + valid in, RGB out)."""
+    from opticalflowfromdepth_amd import ops
+    rgb = (out[:, 0:3] * valid).contiguous()
+    res = ops.inpaint(rgb, valid, coll)  # warm-up (workspace, code paging)
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    for s, e in ev:
+        s.record(stream)
+        res = ops.inpaint(rgb, valid, coll)
+        e.record(stream)
+    torch.cuda.synchronize()
+    ms = sum(s.elapsed_time(e) for s, e in ev) / steps
+    B, _, H, W = rgb.shape
+    px = B * H * W
+    gbs = px * 28 / (ms / 1e3) / 1e9
+    return rgb, res, {
+        "metric": "Mpix/s hole-filled (utils.inpaint, layered Telea r=3, same batch)",
+        "value": round(px / (ms / 1e3) / 1e6, 1), "unit": "Mpix/s", "ms_per_step": round(ms, 3), "steps": steps,
+        "hole_fraction": round(float((valid == 0).float().mean()), 4),
+        "roofline": {"bound": "latency (one launch per hole layer)", "achieved": round(gbs, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 5),
+                     "algorithmic_bytes_per_px": 28},
+        "parity": "bit-exact vs oracle/inpaint_oracle.c layered mode; cv2 Telea parity unpinned (no OpenCV)"}
+
+
+def hole_fill_cpu_baseline(rgb, valid, coll, budget_s, threads):
+    """The reference's hole-fill runs cv2.inpaint(TELEA) per image on the CPU
+    (utils.py:149); timed here as the sequential restatement of that algorithm
+    (oracle/inpaint_oracle.c), OpenMP over images, on a bounded sample."""
+    from oracle import oracle  # test infrastructure: baseline leg only
+    B = rgb.shape[0]
+    n = min(max(threads, 1), B)
+    idx = list(range(n // 2)) + list(range(B - (n - n // 2), B))  # both flow kinds
+    r, v, c = rgb[idx].cpu().numpy(), valid[idx].cpu().numpy(), coll[idx].cpu().numpy()
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        oracle.inpaint(r, v, c, 3, layered=False, nthreads=threads)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    px = reps * n * r.shape[2] * r.shape[3]
+    return {"value": px / el / 1e6, "unit": "Mpix/s", "cores": threads, "kind": "port",
+            "sample": f"{n} warped images (of the {B}-image batch, both flow kinds) x {reps} reps, 768x1024 RGB, "
+                      f"oracle/inpaint_oracle.c sequential Telea (cv2.inpaint restatement), one image per thread, "
+                      f"{el:.1f} s wall"}
 
 
 def main():
@@ -187,8 +238,15 @@ def main():
             pass
 
     cpu = None
+    threads = args.cpu_threads if args.cpu_threads > 0 else min(16, os.cpu_count() or 1)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(obj, flow, depth, args.cpu_seconds, args.cpu_threads)
+        cpu = cpu_baseline(obj, flow, depth, args.cpu_seconds, threads)
+
+    hole = None
+    if rank == 0 and not args.no_hole_fill:  # untimed by the driver's clock contract: after the K steps
+        rgb, _, hole = hole_fill_phase(out[0], out[1], out[2], args.hole_fill_steps, stream)
+        if world == 1 and not args.no_cpu_baseline:
+            hole["cpu_baseline"] = hole_fill_cpu_baseline(rgb, out[1], out[2], args.cpu_seconds, threads)
 
     if rank == 0:
         rec = {
@@ -222,6 +280,7 @@ def main():
                             "algorithmic_bytes_per_px": bytes_per_px,
                             "event_ms_per_call": round(dev_ms, 4)},
             "cpu_baseline": cpu,
+            "hole_fill": hole,
         }
         print(json.dumps(rec), flush=True)
     if world > 1:
