@@ -1,0 +1,492 @@
+"""The reference's preprocess.py around the warp, on device and batched.
+
+Every FW call and every hole-fill here goes through the HIP engine
+(``FW`` -> csrc/ofd_fw.hip, ``utils.inpaint`` -> csrc/ofd_inpaint.hip); the
+flow algebra around them is torch on the same device.  Names, argument
+meaning and the torch CPU RNG draw order follow the reference, so a caller
+switching imports gets the same random parameters for the same seeds:
+
+* ``Plausible``, ``Convert``          -- preprocess.py:184-298
+* ``ConcatFlow``, ``BackFlow``         -- preprocess.py:301-326
+* ``SpecialFlow``, ``augment_flow``    -- preprocess.py:24-182
+* ``PreprocessPlusAugment``            -- preprocess.py:329-506 (per image, writes
+  the same npz files), plus ``PreprocessPlusAugment.run_batch``: B images at a
+  time, every FW / inpaint call batched over the images, the per-image random
+  parameters replayed from each image's seed (``draw_image_params``).
+* ``save_group`` / ``save_augment``    -- the npz layout of preprocess.py:437-476.
+
+Behaviour the reference leaves broken is defined here:
+the stereo branch uses the module's device (the reference reads an undefined
+global ``device``, preprocess.py:353), and the augmented-pair save closes the
+parenthesis that preprocess.py:463 leaves open.
+"""
+from __future__ import annotations
+
+import math
+import os
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+from torch import nn
+
+from . import synth
+from .fw import FW
+from .ops import inpaint
+from .synth import fix_warped_depth, get_random, normalize_depth
+
+AUGMENT_SCHEDULE = (0, 5, 6, 7, 1, 5, 6, 7, 2, 5, 6, 7)  # preprocess.py:454
+N_GROUPS = 5  # preprocess.py:427-432
+_GRAY = ((0.2989, 0.2989, 0.2989), (0.5870, 0.5870, 0.5870), (0.1140, 0.1140, 0.1140))  # :152-154
+
+
+# ---------------------------------------------------------------- Plausible / Convert
+class Plausible:
+    """preprocess.py:184-235."""
+
+    @staticmethod
+    def f():
+        return 1
+
+    @staticmethod
+    def B():
+        return 50
+
+    @staticmethod
+    def K(size, another=False):
+        h, w = size
+        K = torch.tensor([[[0.58, 0, 0.5, 0], [0, 0.58, 0.5, 0], [0, 0, 1, 0], [0, 0, 0, 1]]], dtype=torch.float32)
+        if another:
+            K[:, :2, :2] *= 2
+        K[:, 0, :] *= w
+        K[:, 1, :] *= h
+        return K, torch.linalg.inv(K)
+
+    @staticmethod
+    def random_motion(axisangle_range, axisangle_base, translation_range, translation_base,
+                      another_axisangle=None, another_translation=None):
+        ang = [get_random(math.pi * axisangle_range, math.pi * axisangle_base) for _ in range(3)]
+        mot = [get_random(translation_range, translation_base) for _ in range(3)]
+        axisangle = torch.tensor([[ang]], dtype=torch.float32)
+        translation = torch.tensor([[mot]], dtype=torch.float32)
+        if another_axisangle is not None and another_translation is not None:
+            T = synth._transformation_from_parameters(axisangle + another_axisangle, translation + another_translation)
+        else:
+            T = synth._transformation_from_parameters(axisangle, translation)
+        return T, axisangle, translation
+
+
+class Convert:
+    """preprocess.py:237-298; depth / disparity [1,H,W] or batched [B,1,H,W]."""
+
+    @staticmethod
+    def depth_to_disparity(depth, s=None):
+        """s * B * f / depth with s = get_random(0.3, 0.8, False) (drawn unless given: [B] per image)."""
+        if s is None:
+            s = get_random(0.3, 0.8, random_sign=False)
+        elif torch.is_tensor(s) and s.dim() == 1:
+            s = s.to(depth.device).view(-1, *([1] * (depth.dim() - 1)))
+        return s * Plausible.B() * Plausible.f() / depth
+
+    @staticmethod
+    def disparity_to_flow(disparity, device=None, random_sign=True):
+        cdim = disparity.dim() - 3
+        flow = torch.cat((disparity, torch.zeros_like(disparity)), dim=cdim) * -1.0
+        if random_sign:
+            flow = flow * get_random(0, 1)
+        return flow.to(device) if device is not None else flow
+
+    @staticmethod
+    def disparity_to_depth(disparity):
+        return Plausible.B() * Plausible.f() / (disparity + 0.005)
+
+    @staticmethod
+    def depth_to_random_flow(depth, device=None, segment=None, T1=None):
+        """Ego-motion flow (preprocess.py:265-298, geometry.py:17-67); T1 drawn unless given."""
+        if T1 is None:
+            T1, _, _ = Plausible.random_motion(1. / 36., 1. / 36., 0.1, 0.1)
+        batched = depth.dim() == 4
+        d = depth if batched else depth.unsqueeze(0)
+        T = T1 if T1.dim() == 3 else T1.unsqueeze(0)
+        if T.shape[0] != d.shape[0]:
+            T = T.expand(d.shape[0], 4, 4)
+        flow = synth.ego_motion_flow(d, T.to(d.device))
+        if device is not None:
+            flow = flow.to(device)
+        return (flow if batched else flow[0]), T1
+
+
+# ---------------------------------------------------------------- ConcatFlow / BackFlow
+class ConcatFlow(nn.Module):
+    """preprocess.py:301-313: flowAC = (FW(flowBC, back_flowAB, depthB) + flowAB) * valid."""
+
+    def __init__(self, device=None):
+        super().__init__()
+        self.device = device
+        self.fw = FW(device)
+
+    def forward(self, flowAB, back_flowAB, flowBC, imgB_depth):
+        with torch.no_grad():
+            concat_flow, valid, collision = self.fw(flowBC, back_flowAB, imgB_depth)
+        concat_flow = (concat_flow + flowAB) * valid
+        return concat_flow.to(self.device) if self.device is not None else concat_flow, valid
+
+
+class BackFlow(nn.Module):
+    """preprocess.py:315-326: back flow = -FW(flowAB, flowAB, depthA) * valid."""
+
+    def __init__(self, device=None):
+        super().__init__()
+        self.device = device
+        self.fw = FW(device)
+
+    def forward(self, flowAB, imgA_depth):
+        with torch.no_grad():
+            back_flow, valid, collision = self.fw(flowAB, flowAB, imgA_depth)
+        back_flow = (back_flow * -1.0) * valid
+        return back_flow.to(self.device) if self.device is not None else back_flow, valid
+
+
+# ---------------------------------------------------------------- SpecialFlow
+def _p0(h, w, device):
+    ys, xs = torch.meshgrid(torch.arange(h, device=device), torch.arange(w, device=device), indexing="ij")
+    return xs.to(torch.float32), ys.to(torch.float32)
+
+
+def special_flow_from_params(h, w, kind, params, device) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(special_flow, back_special_flow) [B,2,h,w] for per-image parameters.
+
+    kind 5 = flip (vertical: a fresh SpecialFlow toggles horizontal_flip to
+    False, preprocess.py:49-54), 6 = rotate (params [B,3]: cx, cy, theta),
+    7 = shear (vertical for a fresh instance, :83-91; params [B]: shear).
+    The 2x2 products of :74-75 / :94-95 are evaluated as separate multiplies
+    and adds (no fused multiply-add)."""
+    x, y = _p0(h, w, device)
+    if kind >= 7:
+        s = params.to(device=device, dtype=torch.float32).view(-1, 1, 1)
+        fy = (x * s + y) - y
+        by = (x * (-s) + y) - y
+        zero = torch.zeros_like(fy)
+        return torch.stack((zero, fy), 1), torch.stack((zero, by), 1)
+    if kind >= 6:
+        p = params.to(device=device, dtype=torch.float32)
+        cx, cy, th = p[:, 0].view(-1, 1, 1), p[:, 1].view(-1, 1, 1), p[:, 2]
+        out = []
+        for sgn in (1.0, -1.0):
+            t = th * sgn
+            c, sn = torch.cos(t).view(-1, 1, 1), torch.sin(t).view(-1, 1, 1)
+            dx, dy = x - cx, y - cy
+            px = (dx * c + dy * sn) + cx      # [dx, dy] @ [[c, -s], [s, c]] + c0
+            py = (dx * (-sn) + dy * c) + cy
+            out.append(torch.stack((px - x, py - y), 1))
+        return out[0], out[1]
+    B = params.shape[0] if params is not None else 1
+    fy = (float(h - 1) - y) - y
+    f = torch.stack((torch.zeros_like(fy), fy), 0).unsqueeze(0).expand(B, 2, h, w).contiguous()
+    return f, f.clone()
+
+
+class SpecialFlow(nn.Module):
+    """preprocess.py:24-105 (flip / rotate / shear dense flows, with the
+    instance's alternating flip and shear orientation)."""
+
+    def __init__(self, device=None):
+        super().__init__()
+        self.device = device
+        self.horizontal_flip = True
+        self.horizontal_shear = True
+
+    def forward(self, size, augment_flow_type):
+        h, w = size
+        dev = self.device if self.device is not None else "cpu"
+        if augment_flow_type >= 7.:
+            return self._shear(size)
+        if augment_flow_type >= 6.:
+            c0x = get_random(w / 4, w / 2) + w / 2
+            c0y = get_random(h / 4, h / 2) + h / 2
+            theta = torch.deg2rad(get_random(2, 8))
+            f, b = special_flow_from_params(h, w, 6, torch.stack((c0x, c0y, theta)).view(1, 3), dev)
+            return f[0], b[0]
+        if augment_flow_type >= 5.:
+            self.horizontal_flip = not self.horizontal_flip
+            x, y = _p0(h, w, dev)
+            if self.horizontal_flip:
+                f = torch.stack(((float(w - 1) - x) - x, torch.zeros_like(x)), 0)
+            else:
+                f = torch.stack((torch.zeros_like(y), (float(h - 1) - y) - y), 0)
+            return f, f.clone()
+        raise ValueError(f"SpecialFlow: augment_flow_type {augment_flow_type} < 5")
+
+    def _shear(self, size):
+        h, w = size
+        dev = self.device if self.device is not None else "cpu"
+        self.horizontal_shear = not self.horizontal_shear
+        s = get_random(0.15, 0.2)
+        x, y = _p0(h, w, dev)
+        if self.horizontal_shear:  # p0 @ [[1, 0], [s, 1]]: x' = x + y * s
+            fx, bx = (x + y * s.to(dev)) - x, (x + y * (-s).to(dev)) - x
+            z = torch.zeros_like(fx)
+            return torch.stack((fx, z), 0), torch.stack((bx, z), 0)
+        f, b = special_flow_from_params(h, w, 7, s.view(1), dev)
+        return f[0], b[0]
+
+
+# ---------------------------------------------------------------- augment_flow
+def draw_augment_params(kind: int, h: int, w: int):
+    """The torch CPU RNG draws augment_flow makes for one call of this type
+    (preprocess.py:111, :64-66, :84, :157-162), in order."""
+    if kind >= 7:
+        return get_random(0.15, 0.2)
+    if kind >= 6:
+        c0x = get_random(w / 4, w / 2) + w / 2
+        c0y = get_random(h / 4, h / 2) + h / 2
+        theta = torch.deg2rad(get_random(2, 8))
+        return torch.stack((c0x, c0y, theta)).to(torch.float32)
+    if kind >= 2:  # flip, the unused 3-4 and gray draw nothing
+        return None
+    if kind >= 1:
+        channel = int(get_random(3, 0, False))
+        shift = get_random(10, 15)
+        return (channel, shift)
+    return get_random(1, 0, False)
+
+
+def _stack_params(kind, params: List):
+    if kind >= 7:
+        return torch.stack([p.to(torch.float32) for p in params])
+    if kind >= 6:
+        return torch.stack(params)
+    return None
+
+
+def augment_flow_batch(img0, img0_depth, img1, img1_depth, flow01, back_flow01, kind, params: List,
+                       fw: Optional[FW] = None, specials: Optional[Tuple[torch.Tensor, torch.Tensor]] = None):
+    """augment_flow (preprocess.py:107-182) over a batch: every tensor [B,...],
+    ``params`` the per-image draws of draw_augment_params.  Returns (set1, set2,
+    kind, specials) like the reference (specials None for kinds < 5).
+    ``specials`` optionally supplies the (special, back_special) flows."""
+    fw = fw or FW()
+    cf, bf = ConcatFlow(), BackFlow()
+    B, _, h, w = img0.shape
+    dev = img0.device
+    if kind >= 5:
+        if specials is not None:
+            sf, bsf = specials
+        else:
+            sf, bsf = special_flow_from_params(h, w, kind, _stack_params(kind, params) if kind >= 6 else
+                                               torch.zeros(B), dev)
+        a0_flow, _ = cf(bsf, sf, flow01, img0_depth)
+        a1_flow, _ = cf(flow01, back_flow01, sf, img1_depth)
+        a0_all, valid, coll = fw(torch.cat((img0, img0_depth), 1), sf, img0_depth)
+        a0 = inpaint(a0_all[:, 0:3], valid, coll)
+        a0_depth = fix_warped_depth(a0_all[:, 3:4])
+        a1_all, valid, coll = fw(torch.cat((img1, img1_depth), 1), sf, img1_depth)
+        a1 = inpaint(a1_all[:, 0:3], valid, coll)
+        a1_depth = fix_warped_depth(a1_all[:, 3:4])
+        back_a0_flow, _ = bf(a0_flow, a0_depth)
+        back_a1_flow, _ = bf(a1_flow, img0_depth)
+        return ((a0, a0_depth, a0_flow, back_a0_flow, img1, img1_depth),
+                (img0, img0_depth, a1_flow, back_a1_flow, a1, a1_depth), int(kind), (sf, bsf))
+    if kind >= 3:
+        return None  # preprocess.py:148-149 (`pass`): the reference returns None
+    if kind >= 2:
+        g = torch.tensor(_GRAY, dtype=torch.float32, device=dev)
+        fn = lambda im: (im.permute(0, 2, 3, 1) @ g).permute(0, 3, 1, 2)
+    elif kind >= 1:
+        shift = torch.zeros_like(img0)
+        for b, (ch, v) in enumerate(params):
+            shift[b, ch] = v.to(dev)
+        fn = lambda im: im + shift
+    else:
+        sc = torch.stack([p.to(torch.float32) for p in params]).to(dev).view(-1, 1, 1, 1)
+        fn = lambda im: im * sc
+    return ((fn(img0), img0_depth, flow01, back_flow01, img1, img1_depth),
+            (img0, img0_depth, flow01, back_flow01, fn(img1), img1_depth), int(kind), None)
+
+
+def augment_flow(img0, img0_depth, img1, img1_depth, flow01, back_flow01, device=None, augment_flow_type=None):
+    """Drop-in for preprocess.py:107-182 (3-D inputs), same RNG draws."""
+    _, h, w = img0.shape
+    if augment_flow_type is None:
+        augment_flow_type = get_random(8, 0, False)
+    kind = float(augment_flow_type)
+    p = draw_augment_params(int(kind) if kind < 8 else 7, h, w)
+    if 3. <= kind < 5.:
+        return None
+    res = augment_flow_batch(img0[None], img0_depth[None], img1[None], img1_depth[None], flow01[None],
+                             back_flow01[None], kind, [p])
+    set1, set2, k, spec = res
+    set1 = tuple(t[0] for t in set1)
+    set2 = tuple(t[0] for t in set2)
+    if spec is not None:
+        spec = (spec[0][0], spec[1][0])
+    return set1, set2, k, spec
+
+
+# ---------------------------------------------------------------- per-image RNG replay
+def draw_image_params(seed: int, h: int, w: int, schedule: Sequence[int] = AUGMENT_SCHEDULE,
+                      n_groups: int = N_GROUPS) -> Dict:
+    """Everything PreprocessPlusAugment.forward draws from the torch CPU RNG for
+    one image after utils.set_seed(seed) (preprocess.py:555), in draw order:
+    s (:356 -> :240), T1 (:372 -> :277), then per (group, augment) the draws of
+    augment_flow (:458).  The caller's RNG state is restored afterwards."""
+    state = torch.random.get_rng_state()
+    try:
+        torch.manual_seed(seed)
+        s = get_random(0.3, 0.8, random_sign=False)
+        T1, _, _ = Plausible.random_motion(1. / 36., 1. / 36., 0.1, 0.1)
+        aug = [[draw_augment_params(t, h, w) for t in schedule] for _ in range(n_groups)]
+    finally:
+        torch.random.set_rng_state(state)
+    return {"s": s.to(torch.float32), "T1": T1[0], "augment": aug}
+
+
+# ---------------------------------------------------------------- PreprocessPlusAugment
+class PreprocessPlusAugment(nn.Module):
+    """preprocess.py:329-506: first-stage warps of one image (7 FW calls, 5
+    hole-fills) into the 44-channel group, then 5 x 12 augmentations."""
+
+    def __init__(self, device):
+        super().__init__()
+        self.device = device
+        self.fw = FW(device)
+        self.cf = ConcatFlow(device)
+        self.bf = BackFlow(device)
+
+    # -- the first stage, batched: img0 [B,3,H,W], img0_depth [B,1,H,W] (raw), params per image
+    def stage_one(self, img0, img0_depth, params: List[Dict]):
+        fw, cf = self.fw, self.cf
+        s = torch.stack([p["s"] for p in params])
+        T1 = torch.stack([p["T1"] for p in params])
+        img0_depth = normalize_depth(img0_depth)                                      # :355
+        disp0 = Convert.depth_to_disparity(img0_depth, s)                              # :356
+        flow01 = Convert.disparity_to_flow(disp0, random_sign=False)                   # :357
+        o, img1_valid, coll = fw(torch.cat((img0, img0_depth, flow01 * -1.0), 1), flow01, img0_depth)
+        img1, img1_depth, back_flow01 = o[:, 0:3], o[:, 3:4], o[:, 4:6]
+        img1 = img1 * img1_valid
+        img1_depth = img1_depth * img1_valid
+        back_flow01 = back_flow01 * img1_valid
+        img1_depth = fix_warped_depth(img1_depth)
+        img1 = inpaint(img1, img1_valid, coll)                                         # :366
+
+        flow12, _ = Convert.depth_to_random_flow(img1_depth, T1=T1)                    # :372
+        o, valid, coll = fw(torch.cat((img1, img1_depth, flow12 * -1.0, img1_valid), 1), flow12, img1_depth)
+        img2, img2_depth, back_flow12, fw_img1_valid = o[:, 0:3], o[:, 3:4], o[:, 4:6], o[:, 6:7]
+        img2_valid = valid * fw_img1_valid
+        img2 = img2 * img2_valid
+        img2_depth = img2_depth * img2_valid
+        back_flow12 = back_flow12 * img2_valid
+        img2 = inpaint(img2, img2_valid, coll)
+        img2_depth = fix_warped_depth(img2_depth)
+
+        flow03, _ = Convert.depth_to_random_flow(img0_depth, T1=T1)                    # :385
+        o, img3_valid, coll = fw(torch.cat((img0, img0_depth, flow03 * -1.0), 1), flow03, img0_depth)
+        img3, img3_depth, back_flow03 = o[:, 0:3], o[:, 3:4], o[:, 4:6]
+        img3 = img3 * img3_valid
+        img3_depth = img3_depth * img3_valid
+        back_flow03 = back_flow03 * img3_valid
+        img3 = inpaint(img3, img3_valid, coll)
+        img3_depth = fix_warped_depth(img3_depth)
+
+        flow02, flow02_valid = cf(flow01, back_flow01, flow12, img1_depth)             # :400
+        o, valid, coll = fw(torch.cat((img0, img0_depth, flow02 * -1.0, flow02_valid), 1), flow02, img0_depth)
+        img2p, img2p_depth, back_flow02p, fw_flow02_valid = o[:, 0:3], o[:, 3:4], o[:, 4:6], o[:, 6:7]
+        img2p_valid = valid * fw_flow02_valid
+        img2p = img2p * img2p_valid
+        img2p_depth = img2p_depth * img2p_valid
+        back_flow02p = back_flow02p * img2p_valid
+        img2p = inpaint(img2p, img2p_valid, coll)
+        img2p_depth = fix_warped_depth(img2p_depth)
+
+        flow13, flow13_valid = cf(back_flow01, flow01, flow03, img1_depth)             # :414
+        flow13_valid = flow13_valid * img1_valid
+        o, valid, coll = fw(torch.cat((img1, img1_depth, flow13 * -1.0, flow13_valid), 1), flow13, img1_depth)
+        img3p, img3p_depth, back_flow13p, fw_flow13_valid = o[:, 0:3], o[:, 3:4], o[:, 4:6], o[:, 6:7]
+        img3p_valid = valid * fw_flow13_valid
+        img3p = img3p * img3p_valid
+        img3p_depth = img3p_depth * img3p_valid
+        back_flow13p = back_flow13p * img3p_valid
+        img3p = inpaint(img3p, img3p_valid, coll)
+        img3p_depth = fix_warped_depth(img3p_depth)
+
+        groups = [(img0, img0_depth, img1, img1_depth, flow01, back_flow01),           # :427-432
+                  (img1, img1_depth, img2, img2_depth, flow12, back_flow12),
+                  (img0, img0_depth, img2p, img2p_depth, flow02, back_flow02p),
+                  (img0, img0_depth, img3, img3_depth, flow03, back_flow03),
+                  (img1, img1_depth, img3p, img3p_depth, flow13, back_flow13p)]
+        group44 = torch.cat((img0, img0_depth, img1, img1_depth, img2, img2_depth, img3, img3_depth,
+                             img2p, img2p_depth, img3p, img3p_depth,
+                             flow01, back_flow01, flow12, back_flow12, flow02, back_flow02p,
+                             flow03, back_flow03, flow13, back_flow13p), 1)                # :437-440
+        return group44, groups
+
+    def augment(self, groups, params: List[Dict], schedule: Sequence[int] = AUGMENT_SCHEDULE):
+        """Yields (group_idx, augment_idx, kind, data1 [B,8,H,W], data2 [B,8,H,W]) (preprocess.py:453-476)."""
+        for g, (imgA, dA, imgB, dB, fAB, bAB) in enumerate(groups):
+            for a, kind in enumerate(schedule):
+                set1, set2, _, _ = augment_flow_batch(imgA, dA, imgB, dB, fAB, bAB, kind,
+                                                      [p["augment"][g][a] for p in params], self.fw)
+                yield g, a, kind, torch.cat(set1[0:4], 1), torch.cat(set2[2:6], 1)
+
+    def run_batch(self, seeds: Sequence[int], img0, img0_depth, is_stereo=False, out_dirs=None,
+                  schedule: Sequence[int] = AUGMENT_SCHEDULE, augment=True):
+        """B images at once.  ``img0_depth`` is the raw depth (or the disparity
+        when is_stereo, :352-353).  With ``out_dirs`` every image's npz files
+        are written like the reference; returns the group tensor [B,44,H,W]."""
+        h, w = img0.shape[-2:]
+        params = [draw_image_params(int(s), h, w, schedule) for s in seeds]
+        img0 = img0.to(self.device)
+        d0 = img0_depth.to(self.device)
+        if is_stereo:
+            d0 = Convert.disparity_to_depth(d0)
+        group44, groups = self.stage_one(img0, d0, params)
+        if out_dirs is not None:
+            save_group(out_dirs, group44)
+        if augment:
+            for g, a, kind, d1, d2 in self.augment(groups, params, schedule):
+                if out_dirs is not None:
+                    save_augment(out_dirs, g, a, kind, d1, d2)
+        return group44
+
+    def forward(self, datas, output_dir, is_stereo=False, n_continuous=4):
+        """preprocess.py:341-506 for one image under the caller's current RNG
+        state (the reference seeds with utils.set_seed before each call)."""
+        if not is_stereo:
+            img0, d0 = datas
+        else:
+            img0, _, d0 = datas
+        h, w = img0.shape[-2:]
+        # the draws use the global RNG in the reference's order (see draw_image_params)
+        s = get_random(0.3, 0.8, random_sign=False)
+        T1, _, _ = Plausible.random_motion(1. / 36., 1. / 36., 0.1, 0.1)
+        aug = [[draw_augment_params(t, h, w) for t in AUGMENT_SCHEDULE] for _ in range(N_GROUPS)]
+        params = [{"s": s.to(torch.float32), "T1": T1[0], "augment": aug}]
+        img0 = img0.to(self.device)[None]
+        d0 = d0.to(self.device)[None]
+        if is_stereo:
+            d0 = Convert.disparity_to_depth(d0)
+        os.makedirs(output_dir, exist_ok=True)
+        group44, groups = self.stage_one(img0, d0, params)
+        save_group([output_dir], group44)
+        for g, a, kind, d1, d2 in self.augment(groups, params):
+            save_augment([output_dir], g, a, kind, d1, d2)
+
+
+# ---------------------------------------------------------------- npz writer
+def save_group(out_dirs: Sequence[str], group44: torch.Tensor) -> None:
+    """group.npz, key img_depth_flow = [44,H,W] (preprocess.py:434-447)."""
+    arr = group44.detach().cpu().numpy()
+    for d, x in zip(out_dirs, arr):
+        assert x.shape[0] == 44, "wrong data shape"
+        os.makedirs(d, exist_ok=True)
+        np.savez_compressed(os.path.join(d, "group.npz"), img_depth_flow=x)
+
+
+def save_augment(out_dirs: Sequence[str], g: int, a: int, kind: int, d1: torch.Tensor, d2: torch.Tensor) -> None:
+    """{g}_{a}_1.npz / {g}_{a}_2.npz, keys img_depth_flow [8,H,W] and
+    augment_flow_type (preprocess.py:462-476)."""
+    a1, a2 = d1.detach().cpu().numpy(), d2.detach().cpu().numpy()
+    for d, x1, x2 in zip(out_dirs, a1, a2):
+        assert x1.shape[0] == 8 and x2.shape[0] == 8
+        np.savez_compressed(os.path.join(d, f"{g}_{a}_1.npz"), img_depth_flow=x1, augment_flow_type=kind)
+        np.savez_compressed(os.path.join(d, f"{g}_{a}_2.npz"), img_depth_flow=x2, augment_flow_type=kind)

@@ -208,7 +208,9 @@ def disparity_flow(depth: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
 def ego_motion_flow(depth: torch.Tensor, T: torch.Tensor) -> torch.Tensor:
     """Convert.depth_to_random_flow (preprocess.py:265-298), batched.
 
-    depth [B,1,H,W] float32, T [B,4,4] -> flow [B,2,H,W] float32 on depth's device."""
+    depth [B,1,H,W] (float32, or float64 as the first stage passes it: the
+    product with the camera rays is taken in float64 and then rounded, as
+    geometry.py:39-40 does), T [B,4,4] -> flow [B,2,H,W] float32."""
     B, _, h, w = depth.shape
     dev = depth.device
     K, inv_K = intrinsics(h, w)
@@ -217,8 +219,8 @@ def ego_motion_flow(depth: torch.Tensor, T: torch.Tensor) -> torch.Tensor:
     pix = torch.stack([xs.reshape(-1).float(), ys.reshape(-1).float(),
                        torch.ones(h * w, device=dev)], 0)                       # geometry.py:27-35
     cam = torch.matmul(inv_K[:3, :3], pix).unsqueeze(0)                          # :38
-    cam = depth.reshape(B, 1, -1).to(torch.float32) * cam                        # :39
-    cam = torch.cat([cam, torch.ones(B, 1, h * w, device=dev)], 1)               # :40
+    cam = depth.reshape(B, 1, -1) * cam                                          # :39 (depth's dtype)
+    cam = torch.cat([cam, torch.ones(B, 1, h * w, device=dev, dtype=cam.dtype)], 1).to(torch.float32)  # :40
     P = torch.matmul(K.unsqueeze(0), T.to(dev))[:, :3, :]                        # :57
     cp = torch.matmul(P, cam)                                                    # :59
     pc = cp[:, :2, :] / (cp[:, 2, :].unsqueeze(1) + 1e-7)                        # :61

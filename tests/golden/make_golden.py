@@ -32,6 +32,14 @@ What it does, and what each fixture pins:
   image unchanged.  Pins the keep-mask algebra (:137-142), the HWC uint8 cast
   (:148) and the float32 return (:149-151) with the reference's own code; the
   Telea fill values themselves stay unpinned (OpenCV is absent).
+* ``augment.npz`` -- the reference's own ``SpecialFlow`` / ``augment_flow``
+  (verbatim text slice preprocess.py:24-182), ``ConcatFlow`` / ``BackFlow``
+  (:301-326) and the first stage of ``PreprocessPlusAugment.forward``
+  (:329-450, which ends at the group.npz save; the rest of the file does not
+  parse), run on CPU with the oracle as ``fw_cuda`` and the recording cv2
+  (its ``inpaint`` returns the uint8 image unchanged, so hole pixels are the
+  cast input and only kept pixels pin image values).  Pins the flow algebra,
+  the RNG draw order, the special-flow geometry and the 44-channel layout.
 
 Nothing from /root/reference is copied into the repo: only numeric arrays.
 """
@@ -286,6 +294,68 @@ def make_pipeline_cases(ref_fw, Plausible, Convert, utils_mod):
     return cases
 
 
+def load_reference_preprocess_slices(utils_mod, ref_fw, Convert):
+    """SpecialFlow + augment_flow (:24-182), ConcatFlow + BackFlow (:301-326) and
+    PreprocessPlusAugment through its group save (:329-450), as text slices."""
+    import torch.nn as nn
+    lines = open(os.path.join(REF, "preprocess.py")).read().split("\n")
+    ns = dict(torch=torch, nn=nn, np=np, os=os, sys=sys, time=__import__("time"), math=math,
+              utils=utils_mod, FW=ref_fw.FW, Convert=Convert, device="cpu")
+    for a, b in ((301, 326), (24, 182), (329, 450)):
+        exec(compile("\n".join(lines[a - 1:b]), os.path.join(REF, "preprocess.py"), "exec"), ns)
+    return ns
+
+
+def make_augment_cases(ns, utils_mod):
+    """augment_flow per type, ConcatFlow / BackFlow, and the first stage's group tensor."""
+    import tempfile
+    cases = {}
+    h, w = 40, 56
+    raw = synth_depth(h, w, 4242)
+    d64 = utils_mod.normalize_depth(torch.from_numpy(raw.copy()).unsqueeze(0))        # float64, as get_depth
+    img0 = torch.from_numpy(synth_rgb(h, w, 4242))
+    utils_mod.set_seed(4242)
+    flow01 = ns["Convert"].disparity_to_flow(ns["Convert"].depth_to_disparity(d64), device="cpu", random_sign=False)
+    fw = ns["FW"]("cpu")
+    o, v, c = fw(torch.cat((img0, d64, flow01 * -1.0), 0), flow01, d64)
+    img1, d1, back01 = o[0:3] * v, utils_mod.fix_warped_depth(o[3:4] * v), o[4:6] * v
+    base = {"img0": img0, "d0": d64, "img1": img1, "d1": d1, "flow01": flow01, "back01": back01}
+    for k, t in base.items():
+        cases[f"in/{k}"] = t.numpy()
+    for kind in (0, 1, 2, 5, 6, 7):
+        seed = 777 + kind
+        utils_mod.set_seed(seed)
+        set1, set2, typ, spec = ns["augment_flow"](img0, d64, img1, d1, flow01, back01, device="cpu",
+                                                     augment_flow_type=kind)
+        cases[f"aug{kind}/seed"] = np.array(seed)
+        cases[f"aug{kind}/type"] = np.array(typ)
+        for n, t in enumerate(set1):
+            cases[f"aug{kind}/set1_{n}"] = t.numpy()
+        for n, t in enumerate(set2):
+            cases[f"aug{kind}/set2_{n}"] = t.numpy()
+        if spec is not None:
+            cases[f"aug{kind}/special"] = spec[0].numpy()
+            cases[f"aug{kind}/back_special"] = spec[1].numpy()
+    # ConcatFlow / BackFlow on the disparity pair and a float32 rotation-like flow
+    cf, bf = ns["ConcatFlow"]("cpu"), ns["BackFlow"]("cpu")
+    yy, xx = torch.meshgrid(torch.arange(h, dtype=torch.float32), torch.arange(w, dtype=torch.float32), indexing="ij")
+    fBC = torch.stack((0.05 * (yy - h / 2), -0.04 * (xx - w / 2)), 0)
+    cfo, cfv = cf(flow01, back01, fBC, d1)
+    bfo, bfv = bf(fBC, d1.to(torch.float32))
+    cases.update({"cf/flowBC": fBC.numpy(), "cf/out": cfo.numpy(), "cf/valid": cfv.numpy(),
+                  "bf/out": bfo.numpy(), "bf/valid": bfv.numpy()})
+    # PreprocessPlusAugment first stage (7 FW calls, 5 hole-fills, ConcatFlow) -> group.npz
+    ppa = ns["PreprocessPlusAugment"]("cpu")
+    with tempfile.TemporaryDirectory() as td:
+        utils_mod.set_seed(12399)
+        ppa((img0, torch.from_numpy(raw.copy()).unsqueeze(0)), os.path.join(td, "img"), False)
+        g = np.load(os.path.join(td, "img", "group.npz"))["img_depth_flow"]
+    cases["ppa/seed"] = np.array(12399)
+    cases["ppa/raw_depth"] = raw
+    cases["ppa/group"] = g
+    return cases
+
+
 def make_inpaint_mask_cases(ref_inpaint, rec):
     """utils.inpaint's mask algebra and casts on FW outputs and on masks with collisions."""
     pl = np.load(os.path.join(HERE, "pipeline.npz"))
@@ -331,7 +401,13 @@ def main():
     ref_inpaint, rec = load_reference_inpaint()
     im = make_inpaint_mask_cases(ref_inpaint, rec)
     np.savez_compressed(os.path.join(HERE, "inpaint_mask.npz"), **im)
-    for f in ("fw_op.npz", "fw_wrapper.npz", "pipeline.npz", "inpaint_mask.npz"):
+    # utils with inpaint = the reference's, behind the CPU-device shim
+    utils_mod.inpaint = lambda img, valid, coll: ref_inpaint(img.as_subclass(_CpuImage), valid, coll).as_subclass(
+        torch.Tensor)
+    ns = load_reference_preprocess_slices(utils_mod, ref_fw, Convert)
+    au = make_augment_cases(ns, utils_mod)
+    np.savez_compressed(os.path.join(HERE, "augment.npz"), **au)
+    for f in ("fw_op.npz", "fw_wrapper.npz", "pipeline.npz", "inpaint_mask.npz", "augment.npz"):
         print(f, os.path.getsize(os.path.join(HERE, f)), "bytes")
 
 
