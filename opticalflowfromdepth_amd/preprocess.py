@@ -490,3 +490,53 @@ def save_augment(out_dirs: Sequence[str], g: int, a: int, kind: int, d1: torch.T
         assert x1.shape[0] == 8 and x2.shape[0] == 8
         np.savez_compressed(os.path.join(d, f"{g}_{a}_1.npz"), img_depth_flow=x1, augment_flow_type=kind)
         np.savez_compressed(os.path.join(d, f"{g}_{a}_2.npz"), img_depth_flow=x2, augment_flow_type=kind)
+
+
+# ---------------------------------------------------------------- driver (preprocess.py:508-561)
+def main(argv=None) -> None:
+    """``python -m opticalflowfromdepth_amd.preprocess`` -- the reference's
+    ``__main__`` (preprocess.py:521-561) on synthetic depth maps (the DIML /
+    ReDWeb readers are file I/O, out of scope): the same --gpu / --split /
+    --split_id sharding (shard.shard_range), the same per-image seeds
+    12345 + img_idx + epoch * N over two epochs, the same output tree
+    (<out>/<img_idx + epoch * N>/group.npz and {g}_{a}_{1,2}.npz), B images
+    per batched call.  Under torchrun, --split / --split_id default to the
+    world size / rank (one process per GPU; no collective on the data path)."""
+    import argparse
+    from . import shard
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--dataset", default="synthetic", choices=["synthetic"])
+    ap.add_argument("--n-images", type=int, default=8, help="synthetic dataset size")
+    ap.add_argument("--height", type=int, default=768)
+    ap.add_argument("--width", type=int, default=1024)
+    ap.add_argument("--gpu", default=None, type=int)
+    ap.add_argument("--split", default=None, type=int)
+    ap.add_argument("--split_id", default=None, type=int)
+    ap.add_argument("--epochs", default=2, type=int)
+    ap.add_argument("--batch", default=8, type=int, help="images per batched call")
+    ap.add_argument("--out", default="datasets/AugmentedDatasets/synthetic")
+    ap.add_argument("--no-augment", action="store_true")
+    ap.add_argument("--no-save", action="store_true")
+    a = ap.parse_args(argv)
+    world, rank = int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0"))
+    split = a.split if a.split is not None else world
+    split_id = a.split_id if a.split_id is not None else rank
+    gpu = a.gpu if a.gpu is not None else int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", gpu)
+    torch.cuda.set_device(dev)
+    N, h, w = a.n_images, a.height, a.width
+    start, end = shard.shard_range(N, split, split_id)
+    ppa = PreprocessPlusAugment(dev)
+    for epoch in range(a.epochs):
+        for b0 in range(start, end, a.batch):
+            idx = list(range(b0, min(b0 + a.batch, end)))
+            seeds = [shard.image_seed(i, epoch, N) for i in idx]
+            img0 = synth.synthetic_rgb(seeds, h, w, dev)
+            depth = synth.synthetic_depth(seeds, h, w, dev, dtype=torch.float64)  # utils.get_depth is float64
+            dirs = None if a.no_save else [os.path.join(a.out, str(i + epoch * N)) for i in idx]
+            ppa.run_batch(seeds, img0, depth, out_dirs=dirs, augment=not a.no_augment)
+            print(f"rank {rank}: epoch {epoch} images {idx[0]}..{idx[-1]} done", flush=True)
+
+
+if __name__ == "__main__":
+    main()
