@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--engine", choices=["tile", "split", "atomic"], default="tile")
     ap.add_argument("--no-hole-fill", action="store_true", help="skip the config-3 hole-fill phase")
     ap.add_argument("--hole-fill-steps", type=int, default=5)
+    ap.add_argument("--no-fused", action="store_true", help="skip the fused disparity-warp phase")
     return ap.parse_args()
 
 
@@ -105,6 +106,46 @@ def hole_fill_phase(out, valid, coll, steps, stream):
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 5),
                      "algorithmic_bytes_per_px": 28},
         "parity": "bit-exact vs oracle/inpaint_oracle.c layered mode; cv2 Telea parity unpinned (no OpenCV)"}
+
+
+def fused_disparity_phase(B, H, W, steps, dev, stream):
+    """preprocess.py:356-359 as one fused warp (depth ->
+    disparity -> flow -> splat, obj's depth / flow channels generated in the
+    gather) over B disparity images, next to the same call unfused (torch
+    builds the flow and the 6-channel obj, then forward_warp_flow).
+    Algorithmic bytes: RGB 12 + depth 4 in, 6 channels 24 + valid 4 + coll 4
+    out = 48 B/px."""
+    from opticalflowfromdepth_amd import forward_warp_flow, preprocess as pp, synth, warp_disparity
+    seeds = [12345 + i for i in range(B)]
+    depth = synth.normalize_depth(synth.synthetic_depth(seeds, H, W, dev))
+    rgb = synth.synthetic_rgb(seeds, H, W, dev)
+    s = synth.batch_camera_params(seeds)[0].to(dev)
+
+    def unfused():
+        flow = pp.Convert.disparity_to_flow(pp.Convert.depth_to_disparity(depth, s), random_sign=False)
+        return forward_warp_flow(torch.cat((rgb, depth, flow * -1.0), 1), flow, depth)
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        for a, b in ev:
+            a.record(stream)
+            fn()
+            b.record(stream)
+        torch.cuda.synchronize()
+        return sum(a.elapsed_time(b) for a, b in ev) / steps
+
+    ms = timed(lambda: warp_disparity(rgb, depth, s))
+    ms_unfused = timed(unfused)
+    px = B * H * W
+    gbs = px * 48 / (ms / 1e3) / 1e9
+    return {"metric": "Mpix/s fused depth->disparity->flow->splat (preprocess.py:356-359), C=6 out",
+            "value": round(px / (ms / 1e3) / 1e6, 1), "unit": "Mpix/s", "ms_per_step": round(ms, 4),
+            "unfused_ms_per_step": round(ms_unfused, 4), "images": B, "steps": steps,
+            "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(gbs / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_px": 48},
+            "parity": "bit-exact vs the unfused FW call and the oracle (tests/test_fused.py)"}
 
 
 def hole_fill_cpu_baseline(rgb, valid, coll, budget_s, threads):
@@ -242,6 +283,10 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(obj, flow, depth, args.cpu_seconds, threads)
 
+    fused = None
+    if rank == 0 and not args.no_fused:
+        fused = fused_disparity_phase(B, H, W, 10, dev, stream)
+
     hole = None
     if rank == 0 and not args.no_hole_fill:  # untimed by the driver's clock contract: after the K steps
         rgb, _, hole = hole_fill_phase(out[0], out[1], out[2], args.hole_fill_steps, stream)
@@ -281,6 +326,7 @@ def main():
                             "event_ms_per_call": round(dev_ms, 4)},
             "cpu_baseline": cpu,
             "hole_fill": hole,
+            "fused_disparity": fused,
         }
         print(json.dumps(rec), flush=True)
     if world > 1:

@@ -17,6 +17,10 @@
  *       alt_cuda.fw.FW.forward(obj, flow, depth)  -- alt_cuda/fw.py:19-59,
  *       batched: the meshgrid add / clamp / int64 truncation of fw.py:27-42 is
  *       done inside the kernel, the add in the flow's dtype (fw.py:31).
+ *   ofd_fw_warp_disparity_f32 / _f64depth
+ *       preprocess.py:356-359 (Convert.depth_to_disparity, disparity_to_flow,
+ *       the obj concatenation and the FW call) fused into one warp: the flow
+ *       and obj's depth / flow channels are derived from the depth in-kernel.
  *   ofd_fw_workspace_bytes / ofd_fw_workspace_init
  *       no reference counterpart: the reference allocates its z-buffer `dlut`
  *       per call (fw_cuda_kernel.cu:58); here the caller owns a reusable
@@ -120,6 +124,29 @@ int ofd_fw_forward_warp_flow_f64flow(const float *obj, const double *flow, const
                                      float *output, float *valid, float *collision,
                                      int64_t B, int64_t C, int64_t H, int64_t W,
                                      void *workspace, size_t workspace_bytes, void *stream);
+
+/* Fused depth -> disparity -> flow -> FW: preprocess.py:356-359,
+ *     disp0   = Convert.depth_to_disparity(depth)         (s * 50 * 1 / depth, :239-246)
+ *     flow01  = Convert.disparity_to_flow(disp0, random_sign=False)   (:249-254)
+ *     obj_all = torch.cat((obj[:3], depth, flow01 * -1.0, obj[3:]))   (:358)
+ *     FW(obj_all, flow01, depth)                                      (:359)
+ * without the flow plane or the concatenated obj ever being stored: the flow
+ * is derived from the depth inside the kernels, and output channels 3, 4, 5
+ * (depth, disparity, +0) are generated from the winner's depth.
+ * obj [B,Cobj,H,W] f32 holds the caller's other channels (the RGB image, and
+ * any channels the caller appends, e.g. a validity mask); depth [B,1,H,W] in
+ * float32 or float64 (utils.get_depth returns float64; the disparity and the
+ * flow add are computed in the depth's dtype, exactly as torch promotes them);
+ * s [B] f32 per-image scale (the get_random draw of :240).  Output
+ * [B,Cobj+3,H,W], valid / collision [B,1,H,W].  Bit-identical to
+ * ofd_fw_forward_warp_flow_* on the materialised inputs.  TILE engine only:
+ * requires (Cobj+3)*H*W < 2^30 (OFD_FW_ETOOBIG). */
+int ofd_fw_warp_disparity_f32(const float *obj, int64_t Cobj, const float *depth, const float *s,
+                              float *output, float *valid, float *collision, int64_t B, int64_t H,
+                              int64_t W, void *workspace, size_t workspace_bytes, void *stream);
+int ofd_fw_warp_disparity_f64depth(const float *obj, int64_t Cobj, const double *depth, const float *s,
+                                   float *output, float *valid, float *collision, int64_t B, int64_t H,
+                                   int64_t W, void *workspace, size_t workspace_bytes, void *stream);
 
 #ifdef __cplusplus
 }

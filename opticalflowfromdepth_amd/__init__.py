@@ -7,9 +7,11 @@ gfx950 behind a C ABI (include/ofd_fw.h), with the reference's Python surface:
 * ``FW``               -- drop-in for ``alt_cuda.fw.FW``
 * ``forward_warping``  -- drop-in for the extension op ``fw_cuda.forward_warping``
 * ``forward_warp_flow``-- batched FW core (flow -> splat in one native call)
+* ``warp_disparity``   -- preprocess.py:356-359 fused (depth -> disparity -> flow -> splat)
+* ``inpaint``          -- batched GPU hole-fill replacing ``utils.inpaint``
 """
 from .fw import FW
-from .ops import forward_warp_flow, forward_warping
+from .ops import forward_warp_flow, forward_warping, inpaint, warp_disparity
 
-__all__ = ["FW", "forward_warping", "forward_warp_flow"]
+__all__ = ["FW", "forward_warping", "forward_warp_flow", "warp_disparity", "inpaint"]
 __version__ = "0.1.0"

@@ -51,6 +51,7 @@
 #include <string.h>
 
 #include <mutex>
+#include <type_traits>
 #include <unordered_map>
 
 #include "ofd_fw.h"
@@ -145,6 +146,21 @@ __device__ __forceinline__ void load4(const T *__restrict__ q, T v[4], int n) {
     }
 }
 
+// Coordinate sources whose z-test depth is the separate float32 depth plane
+// and that generate no obj channels.
+#define KEY_DEPTH_FROM_PLANE                                                                            \
+    static constexpr int kGen = 0;                                                                    \
+    template <bool kVec>                                                                              \
+    __device__ __forceinline__ void load4d(int64_t b, int64_t p, V x[4], V y[4], float dk[4], int n,  \
+                                           const float *depth) const {                                \
+        load4<kVec>(b, p, x, y, n);                                                                   \
+        ::load4<kVec>(depth + b * HW + p, dk, n);                                                     \
+    }                                                                                                 \
+    __device__ __forceinline__ float key_depth(int64_t b, int64_t p, const float *depth) const {     \
+        return depth[b * HW + p];                                                                     \
+    }                                                                                                 \
+    __device__ __forceinline__ void gen_all(int64_t, unsigned, float *) const {}
+
 // Coordinate sources: the target of the source at pixel p = j*W + i of image b.
 struct SafeF32 {  // fw_cuda.forward_warping inputs: safe_y, safe_x [B,1,H,W]
     using V = float;
@@ -163,6 +179,7 @@ struct SafeF32 {  // fw_cuda.forward_warping inputs: safe_y, safe_x [B,1,H,W]
     __device__ __forceinline__ void target(int, int, V x, V y, int H, int W, int &tx, int &ty) const {
         target_safe<float>(x, y, H, W, tx, ty);
     }
+    KEY_DEPTH_FROM_PLANE
 };
 
 template <typename F>
@@ -184,6 +201,64 @@ struct FlowCoords {  // FW.forward input: flow [B,2,H,W], ch0 = x, ch1 = y
     __host__ bool vec_ok() const { return uintptr_t(flow) % 16 == 0; }
     __device__ __forceinline__ void target(int i, int j, V x, V y, int H, int W, int &tx, int &ty) const {
         target_flow<F>(i, j, x, y, H, W, tx, ty);
+    }
+    KEY_DEPTH_FROM_PLANE
+};
+
+// Fused depth -> disparity -> flow (preprocess.py:239-254 / :356-359):
+// disparity = s * B * f / depth with s * 50 * 1 in float32 and the division in
+// the depth's dtype; flow = cat(disparity, 0) * -1.0, so the x flow is
+// -disparity and the y flow -0.0; obj = cat(rgb, depth, flow * -1.0).  The
+// flow is never stored: BIN and SPLAT derive it from the depth they load, and
+// SPLAT generates obj's three middle channels (depth, disparity, +0) from the
+// winner's depth.  The z-test key is the float32 depth (fw.py:43).
+template <typename D>
+struct DisparityCoords {
+    using V = D;
+    static constexpr int kGen = 3;
+    const D *depth;
+    const float *s;  // [B] per-image scale
+    int64_t HW;
+    __device__ __forceinline__ D disp(int64_t b, D d) const { return D(s[b] * 50.0f * 1.0f) / d; }
+    __device__ __forceinline__ void load(int64_t b, int64_t p, V &x, V &y) const {
+        x = -disp(b, depth[b * HW + p]);
+        y = -D(0);
+    }
+    template <bool kVec>
+    __device__ __forceinline__ void load4(int64_t b, int64_t p, V x[4], V y[4], int n) const {
+        D d[4];
+        ::load4<kVec>(depth + b * HW + p, d, n);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            x[e] = -disp(b, d[e]);
+            y[e] = -D(0);
+        }
+    }
+    template <bool kVec>
+    __device__ __forceinline__ void load4d(int64_t b, int64_t p, V x[4], V y[4], float dk[4], int n,
+                                           const float *) const {
+        D d[4];
+        ::load4<kVec>(depth + b * HW + p, d, n);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            x[e] = -disp(b, d[e]);
+            y[e] = -D(0);
+            dk[e] = float(d[e]);
+        }
+    }
+    __device__ __forceinline__ float key_depth(int64_t b, int64_t p, const float *) const {
+        return float(depth[b * HW + p]);
+    }
+    // generated obj channels of source w: depth, flow_x * -1.0 = disparity, flow_y * -1.0 = +0
+    __device__ __forceinline__ void gen_all(int64_t b, unsigned w, float g[3]) const {
+        const D d = depth[b * HW + w];
+        g[0] = float(d);
+        g[1] = float(disp(b, d));
+        g[2] = 0.0f;
+    }
+    __host__ bool vec_ok() const { return uintptr_t(depth) % 16 == 0; }
+    __device__ __forceinline__ void target(int i, int j, V x, V y, int H, int W, int &tx, int &ty) const {
+        target_flow<D>(i, j, x, y, H, W, tx, ty);
     }
 };
 
@@ -430,7 +505,7 @@ __device__ __forceinline__ void bin_segment(const Coords &co, const float *__res
             for (int e = 0; e < 4; ++e) {
                 const bool ok = mine_lane && tx[q][e] >= 0;
                 const int64_t p = int64_t(jh + 2 * q) * W + i0 + e;
-                const unsigned long long key = ok ? make_key(depth[b * HW + p], unsigned(p)) : 0ull;
+                const unsigned long long key = ok ? make_key(co.key_depth(b, p, depth), unsigned(p)) : 0ull;
                 wave_run_atomic_min(ws.keys + int64_t(bl) * HW, ok ? ty[q][e] * W + tx[q][e] : -1, key);
                 if (ok) ws.flag[int64_t(bl) * g.ntiles + (ty[q][e] / TH) * g.tilesX + tx[q][e] / TW] = 0u;
             }
@@ -494,9 +569,10 @@ __device__ __forceinline__ void band_major_tile(unsigned lin, int nimg, const Ti
 // planes, gathered from obj right out of the LDS z-buffer.
 struct SplatIO {
     float *valid, *coll;
-    const float *obj;  // kFuse only
-    float *out;        // kFuse only
-    int C;
+    const float *obj;  // kFuse only: [B][Cobj][H][W]
+    float *out;        // kFuse only: [B][C][H][W]
+    int C;             // output channels
+    int Cobj, gen_at;  // obj channels; output channel of the first of Coords::kGen generated ones
 };
 
 // SPLAT launch shape: threads per workgroup, gather targets in flight per
@@ -621,8 +697,7 @@ __device__ __forceinline__ void splat_tile(TileLds &L, unsigned lin, const Coord
                         ii[u] = i;
                         jj[u] = j;
                         const int64_t p = int64_t(j) * W + i;
-                        co.template load4<kVec>(b, p, cx[u], cy[u], W - i);
-                        load4<kVec>(depth + b * HW + p, d[u], W - i);
+                        co.template load4d<kVec>(b, p, cx[u], cy[u], d[u], W - i, depth);
                     }
                 }
             }
@@ -672,9 +747,16 @@ __device__ __forceinline__ void splat_tile(TileLds &L, unsigned lin, const Coord
         // planes and masks are touched once: non-temporal.
         constexpr int kT = Cfg::kGT, kCh = 8;
         const int C = io.C;
-        const float *ob = io.obj + b * int64_t(C) * HW;
+        const float *ob = io.obj + b * int64_t(io.Cobj) * HW;
         float *oo = io.out + b * int64_t(C) * HW;
         const unsigned uHW = unsigned(HW);
+        auto source = [&](int c, unsigned wi) -> float {
+            if (Coords::kGen == 0 || c < io.gen_at) return ob[unsigned(c) * uHW + wi];
+            float g[3];
+            co.gen_all(b, wi, g);
+            if (c < io.gen_at + Coords::kGen) return c == io.gen_at ? g[0] : (c == io.gen_at + 1 ? g[1] : g[2]);
+            return ob[unsigned(c - Coords::kGen) * uHW + wi];
+        };
 #pragma unroll
         for (int k = 0; k < TW * TH / Cfg::kThr; k += kT) {
             unsigned t[kT], w[kT];
@@ -695,13 +777,15 @@ __device__ __forceinline__ void splat_tile(TileLds &L, unsigned lin, const Coord
                     __builtin_nontemporal_store(nowin ? 1.f : 0.f, cb + t[u]);
                 }
             }
+            // channels generated from the winner (Coords::kGen of them at output
+            // channel gen_at; obj supplies the others): one source read per target
             for (int c0 = 0; c0 < C; c0 += kCh) {
                 float o[kT][kCh];
 #pragma unroll
                 for (int u = 0; u < kT; ++u)
 #pragma unroll
                     for (int cc = 0; cc < kCh; ++cc)
-                        o[u][cc] = (w[u] != WIN_NONE && c0 + cc < C) ? ob[unsigned(c0 + cc) * uHW + w[u]] : 0.f;
+                        o[u][cc] = (w[u] != WIN_NONE && c0 + cc < C) ? source(c0 + cc, w[u]) : 0.f;
 #pragma unroll
                 for (int u = 0; u < kT; ++u)
 #pragma unroll
@@ -746,6 +830,11 @@ using SplitCfg = SplatCfg<512, 2, 8>;  // split engine: 4 workgroups / CU, light
 // (tools/probe_tile.py): 512 threads / 2 in flight / 4 per CU 702 us;
 // 512 / 8 / 2 per CU 675; as a persistent kernel 655; 256 threads 715.
 using FusedCfg = SplatCfg<512, 8, 4>;
+// coordinate sources that generate channels carry the generated values and a
+// division per source: 4 targets in flight keeps them inside 128 VGPRs
+using FusedGenCfg = SplatCfg<512, 4, 4>;
+template <typename Coords>
+using FusedCfgFor = typename std::conditional<Coords::kGen == 0, FusedCfg, FusedGenCfg>::type;
 
 template <typename Coords, bool kVec, bool kFuse = false, bool kStamp = false, typename Cfg = SplitCfg>
 __global__ __launch_bounds__(Cfg::kThr, Cfg::kMinW) void splat_kernel(Coords co, const float *__restrict__ depth,
@@ -870,7 +959,7 @@ __global__ __launch_bounds__(kBlock) void splat_atomic_kernel(Coords co, const f
             co.target(i, j, x, y, H, W, tx, ty);
             if (tx >= 0) {
                 t = int(bl * HW) + ty * W + tx;  // chunk-local slot (chunk_px < 2^31)
-                key = make_key(depth[b * HW + p], unsigned(p));
+                key = make_key(co.key_depth(b, p, depth), unsigned(p));
             }
         }
         wave_run_atomic_min(keys, t, key);
@@ -1042,7 +1131,7 @@ unsigned resident_slots(K kernel, int threads) {
     return unsigned(cus) * unsigned(per);
 }
 
-template <typename Coords, bool kVec, typename Cfg = FusedCfg>
+template <typename Coords, bool kVec, typename Cfg = FusedCfgFor<Coords>>
 unsigned persist_grid(unsigned tiles) {
     static const unsigned slots = resident_slots(splat_persist_kernel<Coords, kVec, true, false, Cfg>, Cfg::kThr);
     return tiles < slots ? tiles : slots;
@@ -1056,15 +1145,20 @@ hipEvent_t g_prof_start = nullptr, g_prof_stop = nullptr;
 
 template <typename Coords>
 int run_f32(Coords co, const float *obj, const float *depth, float *out, float *valid, float *coll,
-            int64_t B, int64_t C, int64_t H, int64_t W, void *ws, size_t ws_bytes, hipStream_t st) {
+            int64_t B, int64_t C, int64_t H, int64_t W, void *ws, size_t ws_bytes, hipStream_t st,
+            int gen_at = -1) {
     const int64_t HW = H * W;
+    if (gen_at < 0) gen_at = int(C);
     if (B == 0 || HW == 0) return OFD_FW_OK;
     if (C == 0) return zero_masks(valid, coll, size_t(B * HW) * sizeof(float), st);
     if (!ws || !aligned(ws, 16)) return OFD_FW_EWORKSPACE;
     const size_t per_image = per_image_bytes(H, W);
     const TileGeom g = make_geom(H, W);
     // the tile engine's gathers use 32-bit offsets inside one image
-    const Mode mode = (C * HW < (int64_t(1) << 30)) ? engine_mode() : Mode::Atomic;
+    // Coordinate sources that generate obj channels run on the fused TILE
+    // engine only (the gather is where the channels are generated).
+    if (Coords::kGen > 0 && C * HW >= (int64_t(1) << 30)) return OFD_FW_ETOOBIG;
+    const Mode mode = Coords::kGen > 0 ? Mode::Tile : (C * HW < (int64_t(1) << 30)) ? engine_mode() : Mode::Atomic;
 
     // One slab of G images, shared by both engines (so the all-ones key /
     // flag regions are the same bytes whichever engine ran last).  Chunks are
@@ -1095,7 +1189,7 @@ int run_f32(Coords co, const float *obj, const float *depth, float *out, float *
             if (c == nch - 1 && g_prof_stop) (void)hipEventRecord(g_prof_stop, st);
         } else {
             const ChunkArgs a{slab, b0, int(nb)};
-            const SplatIO io{valid, coll, obj, out, int(C)};
+            const SplatIO io{valid, coll, obj, out, int(C), int(C) - Coords::kGen, gen_at};
             const dim3 bgrid(grid_for(nb * g.nseg, kWaves * kBinSPW));
             if (vec)
                 hipLaunchKernelGGL((bin_kernel<Coords, true, kBinSPW>), bgrid, dim3(kWarpThreads), 0, st, co, depth, a,
@@ -1108,12 +1202,15 @@ int run_f32(Coords co, const float *obj, const float *depth, float *out, float *
                 // fused: a persistent SPLAT gathers the output planes itself (dominant kernel)
                 const unsigned tiles = unsigned(nb * g.ntiles);
                 if (c == 0 && g_prof_start) (void)hipEventRecord(g_prof_start, st);
+                using Cfg = FusedCfgFor<Coords>;
                 if (vec)
-                    hipLaunchKernelGGL((splat_persist_kernel<Coords, true>), dim3(persist_grid<Coords, true>(tiles)),
-                                       dim3(FusedCfg::kThr), 0, st, co, depth, io, a, int(H), int(W), HW, g, nullptr);
+                    hipLaunchKernelGGL((splat_persist_kernel<Coords, true, true, false, Cfg>),
+                                       dim3(persist_grid<Coords, true>(tiles)), dim3(Cfg::kThr), 0, st, co, depth, io,
+                                       a, int(H), int(W), HW, g, nullptr);
                 else
-                    hipLaunchKernelGGL((splat_persist_kernel<Coords, false>), dim3(persist_grid<Coords, false>(tiles)),
-                                       dim3(FusedCfg::kThr), 0, st, co, depth, io, a, int(H), int(W), HW, g, nullptr);
+                    hipLaunchKernelGGL((splat_persist_kernel<Coords, false, true, false, Cfg>),
+                                       dim3(persist_grid<Coords, false>(tiles)), dim3(Cfg::kThr), 0, st, co, depth, io,
+                                       a, int(H), int(W), HW, g, nullptr);
                 if (c == nch - 1 && g_prof_stop) (void)hipEventRecord(g_prof_stop, st);
                 continue;
             }
@@ -1224,6 +1321,33 @@ int ofd_fw_forward_warp_flow_f64flow(const float *obj, const double *flow, const
     FlowCoords<double> co{flow, H * W};
     return run_f32(co, obj, depth, output, valid, collision, B, C, H, W, workspace, workspace_bytes,
                    static_cast<hipStream_t>(stream));
+}
+
+int ofd_fw_warp_disparity_f32(const float *obj, int64_t Cobj, const float *depth, const float *s, float *output,
+                              float *valid, float *collision, int64_t B, int64_t H, int64_t W, void *workspace,
+                              size_t workspace_bytes, void *stream) {
+    if (Cobj < 0) return OFD_FW_EINVAL;
+    const int64_t C = Cobj + 3;
+    if (int rc = check_dims(B, C, H, W)) return rc;
+    if (B * H * W > 0 && (!depth || !s || !valid || !collision || !output || (Cobj > 0 && !obj)))
+        return OFD_FW_EINVAL;
+    DisparityCoords<float> co{depth, s, H * W};
+    return run_f32(co, obj, nullptr, output, valid, collision, B, C, H, W, workspace, workspace_bytes,
+                   static_cast<hipStream_t>(stream), int(Cobj < 3 ? Cobj : 3));
+}
+
+int ofd_fw_warp_disparity_f64depth(const float *obj, int64_t Cobj, const double *depth, const float *s,
+                                   float *output, float *valid, float *collision, int64_t B, int64_t H, int64_t W,
+                                   void *workspace, size_t workspace_bytes, void *stream) {
+    if (Cobj < 0) return OFD_FW_EINVAL;
+    const int64_t C = Cobj + 3;
+    if (int rc = check_dims(B, C, H, W)) return rc;
+    if (B * H * W > 0 && (!depth || !s || !valid || !collision || !output || (Cobj > 0 && !obj)))
+        return OFD_FW_EINVAL;
+    if (!aligned(depth, 8)) return OFD_FW_EALIGN;
+    DisparityCoords<double> co{depth, s, H * W};
+    return run_f32(co, obj, nullptr, output, valid, collision, B, C, H, W, workspace, workspace_bytes,
+                   static_cast<hipStream_t>(stream), int(Cobj < 3 ? Cobj : 3));
 }
 
 int ofd_fw_forward_warping_f64(const double *obj, const double *safe_y, const double *safe_x,

@@ -203,3 +203,52 @@ def inpaint(img: torch.Tensor, valid: torch.Tensor, collision: torch.Tensor, rad
                                        ws.numel() if ws is not None else 0, stream.cuda_stream)
         _native.check(rc, "inpaint")
     return out[0] if squeeze else out
+
+
+def warp_disparity(obj: torch.Tensor, depth: torch.Tensor, s: torch.Tensor,
+                   out: Tuple[torch.Tensor, torch.Tensor, torch.Tensor] = None
+                   ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """preprocess.py:356-359 fused (include/ofd_fw.h ofd_fw_warp_disparity_*):
+
+        flow = Convert.disparity_to_flow(Convert.depth_to_disparity(depth), random_sign=False)
+        FW(torch.cat((obj[:, :3], depth, flow * -1.0, obj[:, 3:]), 1), flow, depth)
+
+    in one native call that never stores the flow or the concatenation.
+    obj [B,Cobj,H,W] float32, depth [B,1,H,W] float32 or float64, s [B] (the
+    per-image draw of preprocess.py:240).  Returns (output [B,Cobj+3,H,W],
+    valid, collision), bit-identical to the unfused FW call.
+    """
+    for x, n in ((obj, "obj"), (depth, "depth")):
+        _check_input(x, n)
+    if obj.dim() != 4 or depth.dim() != 4:
+        raise RuntimeError("warp_disparity expects obj [B,C,H,W] and depth [B,1,H,W]")
+    B, Cobj, H, W = obj.shape
+    if tuple(depth.shape) != (B, 1, H, W):
+        raise RuntimeError(f"depth must have shape {(B, 1, H, W)}, got {tuple(depth.shape)}")
+    if obj.dtype != _F32:
+        raise RuntimeError("warp_disparity expects a float32 obj")
+    if depth.dtype not in (_F32, _F64):
+        raise RuntimeError(f"depth must be float32 or float64, got {depth.dtype}")
+    dev = obj.device
+    if depth.device != dev:
+        raise RuntimeError("obj and depth must be on one device")
+    s = torch.as_tensor(s, dtype=_F32).reshape(-1).to(dev).contiguous()
+    if s.numel() != B:
+        raise RuntimeError(f"s must hold one scale per image ({B}), got {s.numel()}")
+    with torch.cuda.device(dev):
+        stream = torch.cuda.current_stream(dev)
+        if out is None:
+            output = torch.empty(B, Cobj + 3, H, W, dtype=_F32, device=dev)
+            valid = torch.empty(B, 1, H, W, dtype=_F32, device=dev)
+            collision = torch.empty_like(valid)
+        else:
+            output, valid, collision = out
+        nbytes = _ws_bytes(B, H, W, False)
+        ws = workspace(dev, nbytes, stream) if nbytes else None
+        lib = _native.lib()
+        fn = lib.ofd_fw_warp_disparity_f64depth if depth.dtype == _F64 else lib.ofd_fw_warp_disparity_f32
+        rc = fn(obj.data_ptr(), Cobj, depth.data_ptr(), s.data_ptr(), output.data_ptr(), valid.data_ptr(),
+                collision.data_ptr(), B, H, W, ws.data_ptr() if ws is not None else None,
+                ws.numel() if ws is not None else 0, stream.cuda_stream)
+        _native.check(rc, "warp_disparity")
+    return output, valid, collision

@@ -32,7 +32,7 @@ from torch import nn
 
 from . import synth
 from .fw import FW
-from .ops import inpaint
+from .ops import inpaint, warp_disparity
 from .synth import fix_warped_depth, get_random, normalize_depth
 
 AUGMENT_SCHEDULE = (0, 5, 6, 7, 1, 5, 6, 7, 2, 5, 6, 7)  # preprocess.py:454
@@ -361,7 +361,9 @@ class PreprocessPlusAugment(nn.Module):
         img0_depth = normalize_depth(img0_depth)                                      # :355
         disp0 = Convert.depth_to_disparity(img0_depth, s)                              # :356
         flow01 = Convert.disparity_to_flow(disp0, random_sign=False)                   # :357
-        o, img1_valid, coll = fw(torch.cat((img0, img0_depth, flow01 * -1.0), 1), flow01, img0_depth)
+        # :358-359 as one fused warp (depth -> disparity -> flow inside the
+        # kernel; bit-identical to fw(cat(img0, depth, -flow01), flow01, depth))
+        o, img1_valid, coll = warp_disparity(img0.to(torch.float32).contiguous(), img0_depth.contiguous(), s)
         img1, img1_depth, back_flow01 = o[:, 0:3], o[:, 3:4], o[:, 4:6]
         img1 = img1 * img1_valid
         img1_depth = img1_depth * img1_valid

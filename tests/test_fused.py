@@ -1,0 +1,87 @@
+"""Fused depth -> disparity -> flow -> splat (preprocess.py:356-359).
+
+ops.warp_disparity must equal, bit for bit, the unfused sequence the
+reference runs: flow = disparity_to_flow(depth_to_disparity(depth)),
+obj = cat(rgb, depth, -flow[, extra]), FW(obj, flow, depth) -- both through
+this repo's FW and through the CPU oracle.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle
+
+
+def _inputs(B, H, W, dtype, seed, extra=0):
+    from opticalflowfromdepth_amd import synth
+    seeds = [seed + i for i in range(B)]
+    d = synth.normalize_depth(synth.synthetic_depth(seeds, H, W, "cpu", dtype=torch.float64)).to(dtype)
+    rgb = synth.synthetic_rgb(seeds, H, W, "cpu")
+    s = synth.batch_camera_params(seeds)[0]
+    ex = (torch.rand(B, extra, H, W, generator=torch.Generator().manual_seed(seed)) > 0.5).to(torch.float32)
+    return rgb, d, s, ex
+
+
+def _unfused(rgb, d, s, ex):
+    from opticalflowfromdepth_amd import preprocess as pp
+    flow = pp.Convert.disparity_to_flow(pp.Convert.depth_to_disparity(d, s), random_sign=False)
+    obj = torch.cat((rgb, d, flow * -1.0, ex), 1).to(torch.float32)
+    return obj, flow
+
+
+def test_unfused_reference_sequence_on_cpu_matches_fixture_flow():
+    """The unfused sequence used as the expectation is the reference's (pipeline.npz flow01)."""
+    import os
+    from conftest import REPO
+    from opticalflowfromdepth_amd import preprocess as pp, synth
+    g = np.load(os.path.join(REPO, "tests", "golden", "pipeline.npz"))
+    d0 = torch.from_numpy(g["img0/norm_depth"])[None]
+    torch.manual_seed(int(g["img0/seed"]))
+    s = synth.get_random(0.3, 0.8, random_sign=False).view(1)
+    flow = pp.Convert.disparity_to_flow(pp.Convert.depth_to_disparity(d0, s), random_sign=False)
+    assert np.array_equal(flow[0].numpy(), g["img0/flow01"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+@pytest.mark.parametrize("shape,extra", [((3, 48, 64), 0), ((2, 37, 53), 1), ((1, 2, 9), 0), ((2, 96, 128), 2)])
+def test_warp_disparity_bit_exact(dtype, shape, extra):
+    from opticalflowfromdepth_amd import forward_warp_flow, warp_disparity
+    B, H, W = shape
+    rgb, d, s, ex = _inputs(B, H, W, dtype, 100 + H, extra)
+    obj, flow = _unfused(rgb, d, s, ex)
+    dev = torch.device("cuda:0")
+    objd = torch.cat((rgb, ex), 1).to(dev)
+    got = warp_disparity(objd, d.to(dev), s)
+    exp_gpu = forward_warp_flow(obj.to(dev), flow.to(dev), d.to(dev).to(torch.float32))
+    exp_cpu = oracle.fw_flow(obj.numpy(), flow.numpy(), d.to(torch.float32).numpy())
+    for g_, e_, c_, n in zip(got, exp_gpu, exp_cpu, ("output", "valid", "collision")):
+        g_ = g_.cpu().numpy()
+        assert np.array_equal(g_, e_.cpu().numpy()), n
+        assert np.array_equal(g_, c_), n
+
+
+@pytest.mark.gpu
+def test_warp_disparity_obj_without_rgb_and_errors():
+    from opticalflowfromdepth_amd import warp_disparity
+    dev = torch.device("cuda:0")
+    rgb, d, s, ex = _inputs(2, 16, 20, torch.float32, 5)
+    obj, flow = _unfused(rgb[:, :0], d, s, ex)  # Cobj = 0: output = depth, disparity, +0
+    got = warp_disparity(torch.empty(2, 0, 16, 20, device=dev), d.to(dev), s)
+    exp = oracle.fw_flow(obj.numpy(), flow.numpy(), d.numpy())
+    assert all(np.array_equal(g.cpu().numpy(), e) for g, e in zip(got, exp))
+    with pytest.raises(RuntimeError):
+        warp_disparity(rgb.to(dev), d.to(dev), s[:1])
+
+
+@pytest.mark.gpu
+def test_warp_disparity_headline_batch():
+    """64 x 768x1024 float64 depth (utils.get_depth's dtype), every image vs the unfused FW."""
+    from opticalflowfromdepth_amd import forward_warp_flow, warp_disparity
+    dev = torch.device("cuda:0")
+    rgb, d, s, ex = _inputs(64, 768, 1024, torch.float64, 12345)
+    obj, flow = _unfused(rgb, d, s, ex)
+    got = warp_disparity(rgb.to(dev), d.to(dev), s)
+    exp = forward_warp_flow(obj.to(dev), flow.to(dev), d.to(dev).to(torch.float32))
+    for g_, e_ in zip(got, exp):
+        assert torch.equal(g_, e_)
