@@ -51,9 +51,9 @@ constexpr float T_FAR = 1.0e6f;
 // ring: L1 distance to the band); 0 = band (known, 4-adjacent to a hole)
 constexpr unsigned C_HOLE = 0x8000u, C_RING = 0x4000u, C_FAR = 0x2000u, LAY = 0x1FFFu, LAY_INF = 0x1FFFu;
 constexpr int DINF = 0x3FFF;  // distance "infinity" in the transforms (> H + W)
-constexpr int kMaxHW = 8192;  // H + W limit: layers fit 13 bits, bins fit LDS
+constexpr int kMaxHW = 4096;  // H + W limit: layers fit 13 bits, 2 bins per layer fit LDS
 constexpr int kMaxRange = 100;
-constexpr int kMaxBins = kMaxHW + 2 * kMaxRange;
+constexpr int kMaxBins = 2 * kMaxHW + 2 * kMaxRange;
 constexpr int kChanGroup = 4;  // channels accumulated together per window pass
 
 inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
@@ -266,79 +266,10 @@ __device__ __forceinline__ int sample(const Img &m, int y, int x, int c, unsigne
     return int(m.out[c * m.HW + q]);
 }
 
-// Telea colour of hole (y, x) at layer L, channels [c0, c0 + n): the
-// weighted sum over the finalised pixels within `range` (icvTeleaInpaintFMM).
-__device__ void telea_colour(const Img &m, int y, int x, unsigned L, float tij, int range, int c0, int n,
-                             unsigned res[kChanGroup]) {
-    bool in_r, in_l, in_d, in_u;
-    const float t_r = tval<false>(m, y, x + 1, L, in_r), t_l = tval<false>(m, y, x - 1, L, in_l);
-    const float t_d = tval<false>(m, y + 1, x, L, in_d), t_u = tval<false>(m, y - 1, x, L, in_u);
-    float gtx, gty;
-    if (!in_r)
-        gtx = !in_l ? (t_r - t_l) * 0.5f : (t_r - tij);
-    else
-        gtx = !in_l ? (tij - t_l) : 0.f;
-    if (!in_d)
-        gty = !in_u ? (t_d - t_u) * 0.5f : (t_d - tij);
-    else
-        gty = !in_u ? (tij - t_u) : 0.f;
-    float Ia[kChanGroup], Jx[kChanGroup], Jy[kChanGroup];
-#pragma unroll
-    for (int c = 0; c < kChanGroup; ++c) Ia[c] = Jx[c] = Jy[c] = 0.f;
-    float s = 1.0e-20f;
-    const int H = m.H, W = m.W;
-    for (int k = y - range; k <= y + range; ++k) {
-        if (k < 0 || k >= H) continue;
-        // cv2's border shifts (padded k == 1 <-> image row 0, k == rows-2 <-> H-1)
-        const int km = k + (k == 0), kp = k - (k == H - 1);
-        for (int l = x - range; l <= x + range; ++l) {
-            if (l < 0 || l >= W) continue;
-            if ((l - x) * (l - x) + (k - y) * (k - y) > range * range) continue;
-            if (inside<false>(m, k, l, L)) continue;
-            const int lm = l + (l == 0), lp = l - (l == W - 1);
-            const float ry = float(y - k), rx = float(x - l);
-            const float len2 = rx * rx + ry * ry;
-            const float dst = float(1. / (double(len2) * sqrt(double(len2))));
-            const float tkl = m.T[int64_t(k) * W + l];
-            const float lev = float(1. / (1 + fabs(double(tkl - tij))));
-            float dir = rx * gtx + ry * gty;
-            if (fabs(double(dir)) <= 0.01) dir = 0.000001f;
-            const float w = float(fabs(double(dst * lev * dir)));
-            const bool nr = !inside<false>(m, k, l + 1, L), nl = !inside<false>(m, k, l - 1, L);
-            const bool nd = !inside<false>(m, k + 1, l, L), nu = !inside<false>(m, k - 1, l, L);
-            for (int c = 0; c < n; ++c) {
-                const int cc = c0 + c;
-                float gix, giy;
-                if (nr)
-                    gix = nl ? float(sample(m, km, lp + 1, cc, L) - sample(m, km, lm - 1, cc, L)) * 2.0f
-                             : float(sample(m, km, lp + 1, cc, L) - sample(m, km, lm, cc, L));
-                else
-                    gix = nl ? float(sample(m, km, lp, cc, L) - sample(m, km, lm - 1, cc, L)) : 0.f;
-                if (nd)
-                    giy = nu ? float(sample(m, kp + 1, lm, cc, L) - sample(m, km - 1, lm, cc, L)) * 2.0f
-                             : float(sample(m, kp + 1, lm, cc, L) - sample(m, km, lm, cc, L));
-                else
-                    giy = nu ? float(sample(m, kp, lm, cc, L) - sample(m, km - 1, lm, cc, L)) : 0.f;
-                Ia[c] += w * float(sample(m, km, lm, cc, L));
-                Jx[c] -= w * (gix * rx);
-                Jy[c] -= w * (giy * ry);
-            }
-            s += w;
-        }
-    }
-#pragma unroll
-    for (int c = 0; c < kChanGroup; ++c) {
-        const float sat = float(double(Ia[c] / s) +
-                                double(Jx[c] + Jy[c]) / (sqrt(double(Jx[c] * Jx[c] + Jy[c] * Jy[c])) + double(1.0e-20f)) +
-                                double(0.5f));
-        res[c] = sat_u8(sat);
-    }
-}
-
-// telea_colour for range 3 (the reference's inpaintRange) with register
+// The Telea colour for range 3 (the reference's inpaintRange) with register
 // patches: the 9x9 patches of INSIDE flags, distances and channel values
 // around the hole are loaded once (every load independent of the others),
-// then weights and sums are formed in telea_colour's exact (k, l) order, so
+// then weights and sums are formed in cv2's exact (k, l) order (hole_wave), so
 // the result is bit-identical.
 //   kBorder = false: window plus one-pixel halo inside the image, no border
 //     index shifts; every sampled position is then a finalised pixel, so
@@ -460,7 +391,7 @@ __device__ __forceinline__ void telea_pixel_r3(const Img &m, int y, int x, unsig
                              : (nu ? (sc - V[pidx(a - 1, b)]) : 0.f);
                 } else {
                     // cv2's shifted rows / columns: km = k + (k == 0), kp = k - (k == H-1),
-                    // lm = l + (l == 0), lp = l - (l == W-1) (telea_colour)
+                    // lm = l + (l == 0), lp = l - (l == W-1) (hole_wave)
                     const bool t0 = y + a == 0, tH = y + a == H - 1, l0 = x + b == 0, lW = x + b == W - 1;
                     auto Vs = [&](int r0, bool rs, int c0, bool cs) -> float {  // V(r0 + rs, c0 + cs)
                         const float v00 = V[pidx(r0, c0)], v01 = V[pidx(r0, c0 + 1)];
@@ -502,21 +433,32 @@ __device__ __forceinline__ void telea_pixel_r3(const Img &m, int y, int x, unsig
 constexpr int kSortThreads = 256;
 constexpr int kSortSpan = 16384;  // pixels per sort workgroup
 
-__device__ __forceinline__ int bin_of(unsigned cd, int nring) {
+// bins: ring layer l -> l-1; hole layer l -> nring + 2(l-1) for holes the
+// register-patch kernel takes (radius 3, window and halo inside the image),
+// nring + 2(l-1) + 1 for the others (one wave per hole)
+__device__ __forceinline__ bool patch_interior(int64_t e, int64_t HW, int H, int W, bool r3) {
+    const int64_t p = e % HW;
+    const int y = int(p / W), x = int(p - int64_t(y) * W);
+    return r3 && y >= 4 && y < H - 4 && x >= 4 && x < W - 4;
+}
+__device__ __forceinline__ int bin_of(unsigned cd, int nring, int64_t e, int64_t HW, int H, int W, bool r3) {
     const unsigned l = cd & LAY;
-    if (cd & C_HOLE) return l != LAY_INF ? nring + int(l) - 1 : -1;
+    if (cd & C_HOLE)
+        return l != LAY_INF ? nring + 2 * (int(l) - 1) + (patch_interior(e, HW, H, W, r3) ? 0 : 1) : -1;
     if (cd & C_RING) return int(l) - 1;
     return -1;
 }
 
 __global__ __launch_bounds__(kSortThreads) void ip_hist_kernel(const uint16_t *__restrict__ code,
-                                                               unsigned *__restrict__ hist, int64_t total, int nring) {
+                                                               unsigned *__restrict__ hist, int64_t total, int nring,
+                                                               int H, int W, bool r3) {
+    const int64_t HW = int64_t(H) * W;
     __shared__ unsigned h[kMaxBins];
     for (int k = threadIdx.x; k < kMaxBins; k += kSortThreads) h[k] = 0;
     __syncthreads();
     const int64_t beg = int64_t(blockIdx.x) * kSortSpan, end = min(beg + kSortSpan, total);
     for (int64_t e = beg + threadIdx.x; e < end; e += kSortThreads) {
-        const int bin = bin_of(code[e], nring);
+        const int bin = bin_of(code[e], nring, e, HW, H, W, r3);
         if (bin >= 0) atomicAdd(&h[bin], 1u);
     }
     __syncthreads();
@@ -560,13 +502,14 @@ __global__ __launch_bounds__(1024) void ip_scan_kernel(const unsigned *__restric
 __global__ __launch_bounds__(kSortThreads) void ip_scatter_kernel(const uint16_t *__restrict__ code,
                                                                   unsigned *__restrict__ cursor,
                                                                   uint32_t *__restrict__ list, int64_t total,
-                                                                  int nring) {
+                                                                  int nring, int H, int W, bool r3) {
+    const int64_t HW = int64_t(H) * W;
     __shared__ unsigned h[kMaxBins];
     for (int k = threadIdx.x; k < kMaxBins; k += kSortThreads) h[k] = 0;
     __syncthreads();
     const int64_t beg = int64_t(blockIdx.x) * kSortSpan, end = min(beg + kSortSpan, total);
     for (int64_t e = beg + threadIdx.x; e < end; e += kSortThreads) {
-        const int bin = bin_of(code[e], nring);
+        const int bin = bin_of(code[e], nring, e, HW, H, W, r3);
         if (bin >= 0) atomicAdd(&h[bin], 1u);
     }
     __syncthreads();
@@ -574,7 +517,7 @@ __global__ __launch_bounds__(kSortThreads) void ip_scatter_kernel(const uint16_t
         if (h[k]) h[k] = atomicAdd(&cursor[k], h[k]);  // this workgroup's range of bin k
     __syncthreads();
     for (int64_t e = beg + threadIdx.x; e < end; e += kSortThreads) {
-        const int bin = bin_of(code[e], nring);
+        const int bin = bin_of(code[e], nring, e, HW, H, W, r3);
         if (bin >= 0) list[atomicAdd(&h[bin], 1u)] = uint32_t(e);
     }
 }
@@ -626,28 +569,122 @@ __global__ __launch_bounds__(256) void ip_negate_kernel(float *__restrict__ T, c
 }
 
 // hole layer L: distance, then every channel's Telea colour
-__global__ __launch_bounds__(256) void ip_hole_layer_kernel(Chunk ch, const uint32_t *__restrict__ list, unsigned n,
-                                                            unsigned L, int range) {
-    const unsigned i = blockIdx.x * 256u + threadIdx.x;
+__device__ __forceinline__ void hole_patch(const Chunk &ch, const uint32_t *__restrict__ list, unsigned n, unsigned i,
+                                           unsigned L) {
     if (i >= n) return;
     int y, x;
     int64_t p;
     const Img m = image_of(ch, list[i], y, x, p);
-    if (range == 3) {
-        if (y >= 4 && y < m.H - 4 && x >= 4 && x < m.W - 4)
-            telea_pixel_r3<false>(m, y, x, L, p);
-        else
-            telea_pixel_r3<true>(m, y, x, L, p);
-        return;
-    }
-    const float t = fm_dist<false>(m, y, x, L);
-    m.T[p] = t;
+    telea_pixel_r3<false>(m, y, x, L, p);  // the sort put only radius-3 interior holes here
+}
+
+// The other holes (image border, or a radius other than 3): one wave per
+// hole.  Lane j evaluates position j of the (2r+1)^2 window raster (64 at a
+// time) -- flags, distance, weight and its channel terms, all loads
+// independent -- and the wave folds the terms in raster order with readlane,
+// so every sum is the sequential one (icvTeleaInpaintFMM's (k, l) loop), bit
+// for bit.
+__device__ __forceinline__ float rl(float v, int j) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
+}
+
+__device__ __forceinline__ void hole_wave(const Chunk &ch, const uint32_t *__restrict__ list, unsigned n, unsigned i,
+                                          unsigned L, int range) {
+    if (i >= n) return;  // wave-uniform
+    const int lane = threadIdx.x & 63;
+    int y, x;
+    int64_t p;
+    const Img m = image_of(ch, list[i], y, x, p);
+    const int H = m.H, W = m.W, R = range, D = 2 * range + 1, npos = D * D;
+    const float tij = fm_dist<false>(m, y, x, L);
+    bool in_r, in_l, in_d, in_u;
+    const float t_r = tval<false>(m, y, x + 1, L, in_r), t_l = tval<false>(m, y, x - 1, L, in_l);
+    const float t_d = tval<false>(m, y + 1, x, L, in_d), t_u = tval<false>(m, y - 1, x, L, in_u);
+    float gtx, gty;
+    if (!in_r)
+        gtx = !in_l ? (t_r - t_l) * 0.5f : (t_r - tij);
+    else
+        gtx = !in_l ? (tij - t_l) : 0.f;
+    if (!in_d)
+        gty = !in_u ? (t_d - t_u) * 0.5f : (t_d - tij);
+    else
+        gty = !in_u ? (tij - t_u) : 0.f;
     for (int c0 = 0; c0 < m.C; c0 += kChanGroup) {
         const int nc = min(kChanGroup, m.C - c0);
-        unsigned res[kChanGroup];
-        telea_colour(m, y, x, L, t, range, c0, nc, res);
-        for (int c = 0; c < nc; ++c) m.out[(c0 + c) * m.HW + p] = float(res[c]);
+        float Ia[kChanGroup], Jx[kChanGroup], Jy[kChanGroup];
+#pragma unroll
+        for (int c = 0; c < kChanGroup; ++c) Ia[c] = Jx[c] = Jy[c] = 0.f;
+        float s = 1.0e-20f;
+        for (int base = 0; base < npos; base += 64) {
+            const int idx = base + lane;
+            const int k = y - R + idx / D, l = x - R + idx % D;
+            bool valid = idx < npos && k >= 0 && k < H && l >= 0 && l < W && (l - x) * (l - x) + (k - y) * (k - y) <= R * R;
+            valid = valid && !inside<false>(m, k, l, L);
+            float w = 0.f, ti[kChanGroup], tx[kChanGroup], ty[kChanGroup];
+#pragma unroll
+            for (int c = 0; c < kChanGroup; ++c) ti[c] = tx[c] = ty[c] = 0.f;
+            if (valid) {
+                const int km = k + (k == 0), kp = k - (k == H - 1), lm = l + (l == 0), lp = l - (l == W - 1);
+                const float ry = float(y - k), rx = float(x - l);
+                const float len2 = rx * rx + ry * ry;
+                const float dst = float(1. / (double(len2) * sqrt(double(len2))));
+                const float lev = float(1. / (1 + fabs(double(m.T[int64_t(k) * W + l] - tij))));
+                float dir = rx * gtx + ry * gty;
+                if (fabs(double(dir)) <= 0.01) dir = 0.000001f;
+                w = float(fabs(double(dst * lev * dir)));
+                const bool nr = !inside<false>(m, k, l + 1, L), nl = !inside<false>(m, k, l - 1, L);
+                const bool nd = !inside<false>(m, k + 1, l, L), nu = !inside<false>(m, k - 1, l, L);
+                for (int c = 0; c < nc; ++c) {
+                    const int cc = c0 + c;
+                    float gix, giy;
+                    if (nr)
+                        gix = nl ? float(sample(m, km, lp + 1, cc, L) - sample(m, km, lm - 1, cc, L)) * 2.0f
+                                 : float(sample(m, km, lp + 1, cc, L) - sample(m, km, lm, cc, L));
+                    else
+                        gix = nl ? float(sample(m, km, lp, cc, L) - sample(m, km, lm - 1, cc, L)) : 0.f;
+                    if (nd)
+                        giy = nu ? float(sample(m, kp + 1, lm, cc, L) - sample(m, km - 1, lm, cc, L)) * 2.0f
+                                 : float(sample(m, kp + 1, lm, cc, L) - sample(m, km, lm, cc, L));
+                    else
+                        giy = nu ? float(sample(m, kp, lm, cc, L) - sample(m, km - 1, lm, cc, L)) : 0.f;
+                    ti[c] = w * float(sample(m, km, lm, cc, L));
+                    tx[c] = w * (gix * rx);
+                    ty[c] = w * (giy * ry);
+                }
+            }
+            const uint64_t vm = __ballot(valid);
+            for (int j = 0; j < 64; ++j) {
+                if (!((vm >> j) & 1ull)) continue;  // uniform
+                for (int c = 0; c < nc; ++c) {
+                    Ia[c] += rl(ti[c], j);
+                    Jx[c] -= rl(tx[c], j);
+                    Jy[c] -= rl(ty[c], j);
+                }
+                s += rl(w, j);
+            }
+        }
+        if (lane == 0) {
+            for (int c = 0; c < nc; ++c) {
+                const float sat = float(double(Ia[c] / s) +
+                                        double(Jx[c] + Jy[c]) / (sqrt(double(Jx[c] * Jx[c] + Jy[c] * Jy[c])) + double(1.0e-20f)) +
+                                        double(0.5f));
+                m.out[(c0 + c) * m.HW + p] = float(sat_u8(sat));
+            }
+        }
     }
+    if (lane == 0) m.T[p] = tij;
+}
+
+// One launch per hole layer: blocks [0, nbp) take the patch-interior holes
+// (thread per hole), the rest the others (wave per hole).  The two sets of a
+// layer are independent, so they share the launch; every block runs one path.
+__global__ __launch_bounds__(256) void ip_hole_layer_kernel(Chunk ch, const uint32_t *__restrict__ lp, unsigned np,
+                                                            unsigned nbp, const uint32_t *__restrict__ lw, unsigned nw,
+                                                            unsigned L, int range) {
+    if (blockIdx.x < nbp)
+        hole_patch(ch, lp, np, blockIdx.x * 256u + threadIdx.x, L);
+    else
+        hole_wave(ch, lw, nw, (blockIdx.x - nbp) * 4u + (threadIdx.x >> 6), L, range);
 }
 
 inline unsigned blocks_for(unsigned n, unsigned per) { return (n + per - 1) / per; }
@@ -684,7 +721,7 @@ int ofd_inpaint_telea_f32(const float *img, const float *valid, const float *col
     unsigned *hist = reinterpret_cast<unsigned *>(workspace);
     unsigned *cursor = reinterpret_cast<unsigned *>(static_cast<char *>(workspace) + align256(size_t(kMaxBins) * 4));
     const IpWs w = carve(static_cast<char *>(workspace) + fixed, G, HW);
-    const int nbins = nring + int(H + W);
+    const int nbins = nring + 2 * int(H + W);
     unsigned hh[kMaxBins];
     for (int64_t b0 = 0; b0 < B; b0 += G) {
         const int64_t nb = B - b0 < G ? B - b0 : G;
@@ -698,14 +735,15 @@ int ofd_inpaint_telea_f32(const float *img, const float *valid, const float *col
         hipError_t e = hipMemsetAsync(hist, 0, size_t(kMaxBins) * 4, st);
         if (e != hipSuccess) return int(e);
         const unsigned sblocks = unsigned((total + kSortSpan - 1) / kSortSpan);
-        hipLaunchKernelGGL(ip_hist_kernel, dim3(sblocks), dim3(kSortThreads), 0, st, w.code, hist, total, nring);
+        hipLaunchKernelGGL(ip_hist_kernel, dim3(sblocks), dim3(kSortThreads), 0, st, w.code, hist, total, nring,
+                           int(H), int(W), r == 3);
         hipLaunchKernelGGL(ip_scan_kernel, dim3(1), dim3(1024), 0, st, hist, cursor, nbins);
         // the layer counts size the per-layer launches: one host round trip per chunk
         e = hipMemcpyAsync(hh, hist, size_t(nbins) * 4, hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipStreamSynchronize(st);
         if (e != hipSuccess) return int(e);
         hipLaunchKernelGGL(ip_scatter_kernel, dim3(sblocks), dim3(kSortThreads), 0, st, w.code, cursor, w.list, total,
-                           nring);
+                           nring, int(H), int(W), r == 3);
         const Chunk ch{w.code, w.T, img, out, int(C), int(H), int(W), HW, b0};
         unsigned off = 0;
         for (int L = 1; L < nring; ++L) {  // outer band, then negated
@@ -718,12 +756,13 @@ int ofd_inpaint_telea_f32(const float *img, const float *valid, const float *col
         off += hh[nring - 1];  // always empty (ring layers stop at 2r - 1)
         if (off)
             hipLaunchKernelGGL(ip_negate_kernel, dim3(blocks_for(off, 256)), dim3(256), 0, st, w.T, w.list, off);
-        for (int L = 1; nring + L - 1 < nbins; ++L) {  // holes
-            const unsigned n = hh[nring + L - 1];
-            if (n)
-                hipLaunchKernelGGL(ip_hole_layer_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, st, ch, w.list + off,
-                                   n, unsigned(L), r);
-            off += n;
+        for (int L = 1; nring + 2 * (L - 1) < nbins; ++L) {  // holes: patch-interior, then the others
+            const unsigned ni = hh[nring + 2 * (L - 1)], nw = hh[nring + 2 * (L - 1) + 1];
+            const unsigned nbp = blocks_for(ni, 256), nbw = blocks_for(nw, 4);
+            if (nbp + nbw)
+                hipLaunchKernelGGL(ip_hole_layer_kernel, dim3(nbp + nbw), dim3(256), 0, st, ch, w.list + off, ni, nbp,
+                                   w.list + off + ni, nw, unsigned(L), r);
+            off += ni + nw;
         }
     }
     const hipError_t e = hipGetLastError();

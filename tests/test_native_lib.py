@@ -87,7 +87,7 @@ def test_inpaint_argument_errors_without_gpu():
     assert f(*([None] * 4), 1, 3, 8, 8, 3, None, 0, None) == -1       # null pointers
     p = ctypes.c_void_p(16)                                            # never dereferenced
     assert f(p, p, p, p, 1, 3, 1, 8, 3, None, 0, None) == -1          # H < 2
-    assert f(p, p, p, p, 1, 3, 4096, 4097, 3, None, 0, None) == -2   # H + W > 8192
+    assert f(p, p, p, p, 1, 3, 2048, 2049, 3, None, 0, None) == -2   # H + W > 4096
     assert f(p, p, p, p, 1, 3, 8, 8, 3, None, 0, None) == -3          # no workspace
     one = lib.ofd_inpaint_workspace_bytes(1, 768, 1024)
     assert one >= 768 * 1024 * 14
