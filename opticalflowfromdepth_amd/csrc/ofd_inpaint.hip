@@ -23,7 +23,7 @@
 //          hole bits, out = float(uint8(img)) for every pixel.
 //   COLS   one thread per column: vertical distances to the nearest known /
 //          hole pixel (two sweeps).
-//   ROWS   one thread per row: the row pass of both L1 distance transforms,
+//   ROWS   one wave per row (prefix / suffix scans): the row pass of both L1 distance transforms,
 //          the Chebyshev-radius test of the outer band; writes the per-pixel
 //          code (hole layer / band / ring layer / far) and initial T.
 //   SORT   chip-wide counting sort of ring pixels and holes by layer (LDS
@@ -154,46 +154,107 @@ __global__ __launch_bounds__(256) void ip_cols_kernel(const uint16_t *__restrict
 // ---------------------------------------------------------------- ROWS
 // Row pass of the L1 distance transforms, d(x) = min_x' g(x') + |x - x'|,
 // and the outer-band test "a hole within Chebyshev distance r" = some x' in
-// [x - r, x + r] with vertical hole distance <= r.  tmp = forward results.
-__global__ __launch_bounds__(64) void ip_rows_kernel(uint16_t *__restrict__ code, float *__restrict__ T,
-                                                     const uint32_t *__restrict__ gcol, uint32_t *__restrict__ tmp,
-                                                     int H, int W, int r) {
-    const int y = blockIdx.x * 64 + threadIdx.x;
-    if (y >= H) return;
+// [x - r, x + r] with vertical hole distance <= r.  One wave per row, 64
+// columns per step (coalesced), using the closed forms of the two sweeps:
+//   forward  f(x) = x + min_{x' <= x} (g(x') - x')     (prefix min)
+//   backward d(x) = -x + min_{x' >= x} (f(x') + x')    (suffix min)
+// and, for the band test, the last / next column x' with g_hole(x') <= r
+// (prefix max / suffix min).  tmp holds the forward results.
+constexpr int kBig = 1 << 28;
+
+__device__ __forceinline__ int wave_prefix_min(int v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int o = __shfl_up(v, d);
+        if (lane >= d) v = min(v, o);
+    }
+    return v;
+}
+__device__ __forceinline__ int wave_prefix_max(int v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int o = __shfl_up(v, d);
+        if (lane >= d) v = max(v, o);
+    }
+    return v;
+}
+__device__ __forceinline__ int wave_suffix_min(int v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int o = __shfl_down(v, d);
+        if (lane + d < 64) v = min(v, o);
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(256) void ip_rows_kernel(uint16_t *__restrict__ code, float *__restrict__ T,
+                                                      const uint32_t *__restrict__ gcol, uint32_t *__restrict__ tmp,
+                                                      int H, int W, int r) {
+    const int y = blockIdx.x * 4 + int(threadIdx.x >> 6);
+    if (y >= H) return;  // wave-uniform
+    const int lane = threadIdx.x & 63;
     const int64_t HW = int64_t(H) * W, bl = blockIdx.y;
     const int64_t row = bl * HW + int64_t(y) * W;
-    int fk = DINF, fh = DINF, lastok = -2 * DINF;
-    for (int x = 0; x < W; ++x) {
-        const uint32_t g = gcol[row + x];
-        const int gk = int(g & 0xFFFFu), gh = int(g >> 16);
-        fk = min(gk, fk + 1);
-        fh = min(gh, fh + 1);
-        if (gh <= r) lastok = x;
-        tmp[row + x] = uint32_t(fk) | (uint32_t(fh) << 16) | (x - lastok <= r ? 0x80000000u : 0u);
-    }
-    int bk = DINF, bh = DINF, nextok = 2 * DINF;
-    for (int x = W - 1; x >= 0; --x) {
-        const uint32_t f = tmp[row + x];
-        const uint32_t g = gcol[row + x];
-        bk = min(int(f & 0x7FFFu), bk + 1);
-        bh = min(int((f >> 16) & 0x7FFFu), bh + 1);
-        if (int(g >> 16) <= r) nextok = x;
-        const bool near = (f >> 31) || nextok - x <= r;
-        const bool hole = code[row + x] & C_HOLE;
-        unsigned cd;
-        float t = T_FAR;
-        if (hole) {
-            cd = C_HOLE | unsigned(bk >= int(LAY_INF) ? LAY_INF : bk);
-        } else if (bh == 1) {
-            cd = 0u;  // band
-            t = 0.f;
-        } else if (near && bh < DINF) {
-            cd = C_RING | unsigned(bh - 1);
-        } else {
-            cd = C_FAR;
+    int ck = kBig, ch = kBig, cl = -kBig;
+    for (int x0 = 0; x0 < W; x0 += 64) {
+        const int x = x0 + lane;
+        int vk = kBig, vh = kBig, lo = -kBig;
+        if (x < W) {
+            const uint32_t g = gcol[row + x];
+            const int gk = int(g & 0xFFFFu), gh = int(g >> 16);
+            vk = gk - x;
+            vh = gh - x;
+            lo = gh <= r ? x : -kBig;
         }
-        code[row + x] = uint16_t(cd);
-        T[row + x] = t;
+        vk = min(wave_prefix_min(vk), ck);
+        vh = min(wave_prefix_min(vh), ch);
+        lo = max(wave_prefix_max(lo), cl);
+        ck = __shfl(vk, 63);
+        ch = __shfl(vh, 63);
+        cl = __shfl(lo, 63);
+        if (x < W)
+            tmp[row + x] = uint32_t(x + vk) | (uint32_t(x + vh) << 16) | (x - lo <= r ? 0x80000000u : 0u);
+    }
+    int sk = kBig, sh = kBig, sn = kBig;
+    for (int x0 = ((W - 1) / 64) * 64; x0 >= 0; x0 -= 64) {
+        const int x = x0 + lane;
+        int uk = kBig, uh = kBig, nx = kBig;
+        uint32_t f = 0;
+        if (x < W) {
+            f = tmp[row + x];
+            const uint32_t g = gcol[row + x];
+            uk = int(f & 0x7FFFu) + x;
+            uh = int((f >> 16) & 0x7FFFu) + x;
+            nx = int(g >> 16) <= r ? x : kBig;
+        }
+        uk = min(wave_suffix_min(uk), sk);
+        uh = min(wave_suffix_min(uh), sh);
+        nx = min(wave_suffix_min(nx), sn);
+        sk = __shfl(uk, 0);
+        sh = __shfl(uh, 0);
+        sn = __shfl(nx, 0);
+        if (x < W) {
+            const int bk = uk - x, bh = uh - x;
+            const bool near = (f >> 31) || nx - x <= r;
+            const bool hole = code[row + x] & C_HOLE;
+            unsigned cd;
+            float t = T_FAR;
+            if (hole) {
+                cd = C_HOLE | unsigned(bk >= int(LAY_INF) ? LAY_INF : bk);
+            } else if (bh == 1) {
+                cd = 0u;  // band
+                t = 0.f;
+            } else if (near && bh < DINF) {
+                cd = C_RING | unsigned(bh - 1);
+            } else {
+                cd = C_FAR;
+            }
+            code[row + x] = uint16_t(cd);
+            T[row + x] = t;
+        }
     }
 }
 
@@ -730,7 +791,7 @@ int ofd_inpaint_telea_f32(const float *img, const float *valid, const float *col
                            dim3(256), 0, st, img, valid, collision, out, w.code, int(C), int(H), int(W), b0);
         hipLaunchKernelGGL(ip_cols_kernel, dim3(unsigned((W + 255) / 256), unsigned(nb)), dim3(256), 0, st, w.code,
                            w.gcol, int(H), int(W));
-        hipLaunchKernelGGL(ip_rows_kernel, dim3(unsigned((H + 63) / 64), unsigned(nb)), dim3(64), 0, st, w.code, w.T,
+        hipLaunchKernelGGL(ip_rows_kernel, dim3(unsigned((H + 3) / 4), unsigned(nb)), dim3(256), 0, st, w.code, w.T,
                            w.gcol, w.list, int(H), int(W), r);
         hipError_t e = hipMemsetAsync(hist, 0, size_t(kMaxBins) * 4, st);
         if (e != hipSuccess) return int(e);
