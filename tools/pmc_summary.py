@@ -13,12 +13,18 @@ import sys
 from collections import OrderedDict
 
 
+WARP_KERNELS = ("bin_kernel", "splat_persist_kernel", "splat_kernel", "resolve2d_kernel", "splat_atomic_kernel",
+                "resolve_atomic_kernel")
+
+
 def per_dispatch(d):
     rows = list(csv.DictReader(open(f"{d}/run_counter_collection.csv")))
     out = OrderedDict()
     for r in rows:
         name = r["Kernel_Name"]
         if "anonymous namespace)::" not in name or "at::" in name:
+            continue
+        if not any(k in name for k in WARP_KERNELS):  # the warp's kernels only
             continue
         k = r["Dispatch_Id"]
         short = name.split("::")[1].split("(")[0].split("<")[0]
