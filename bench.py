@@ -50,6 +50,7 @@ def parse():
     ap.add_argument("--no-hole-fill", action="store_true", help="skip the config-3 hole-fill phase")
     ap.add_argument("--hole-fill-steps", type=int, default=5)
     ap.add_argument("--no-fused", action="store_true", help="skip the fused disparity-warp phase")
+    ap.add_argument("--no-bf16", action="store_true", help="skip the config-5 bf16 warp phase")
     return ap.parse_args()
 
 
@@ -146,6 +147,46 @@ def fused_disparity_phase(B, H, W, steps, dev, stream):
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(gbs / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_px": 48},
             "parity": "bit-exact vs the unfused FW call and the oracle (tests/test_fused.py)"}
+
+
+def bf16_warp_phase(B, H, W, steps, dev, stream):
+    """the training-loop warp on bf16
+    planes (no reference counterpart), at 368x560, next to the float32 warp of
+    the same batch.  Algorithmic bytes at C=6: obj 12 + flow 8 + depth 4 in,
+    output 12 + valid 4 + coll 4 out = 44 B/px (68 for the float32 op)."""
+    from opticalflowfromdepth_amd import forward_warp_flow, synth
+    seeds = [7000 + i for i in range(B)]
+    obj, flow, depth = synth.stage_one_batch(seeds, H, W, dev)
+    objb = obj.to(torch.bfloat16)
+    C = obj.shape[1]
+    outb = (torch.empty_like(objb), torch.empty_like(depth), torch.empty_like(depth))
+    outf = (torch.empty_like(obj), torch.empty_like(depth), torch.empty_like(depth))
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        for a, b in ev:
+            a.record(stream)
+            fn()
+            b.record(stream)
+        torch.cuda.synchronize()
+        return sum(a.elapsed_time(b) for a, b in ev) / steps
+
+    ms = timed(lambda: forward_warp_flow(objb, flow, depth, out=outb))
+    ms_f32 = timed(lambda: forward_warp_flow(obj, flow, depth, out=outf))
+    same = bool(torch.equal(outb[0].view(torch.int16), outf[0].to(torch.bfloat16).view(torch.int16)))
+    px = B * H * W
+    bpp = 4 * C + 20
+    gbs = px * bpp / (ms / 1e3) / 1e9
+    return {"metric": f"Mpix/s bf16 forward warp (config 5, {H}x{W}), C={C}", "value": round(px / (ms / 1e3) / 1e6, 1),
+            "unit": "Mpix/s", "ms_per_step": round(ms, 4), "f32_ms_per_step": round(ms_f32, 4), "images": B,
+            "steps": steps, "dtype": "bf16 planes, f32 flow / depth",
+            "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(gbs / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_px": bpp,
+                         "scope": "whole call (BIN + SPLAT)"},
+            "equals_f32_path": same,
+            "parity": "bit-exact vs the oracle and the float32 path (tests/test_bf16.py)"}
 
 
 def hole_fill_cpu_baseline(rgb, valid, coll, budget_s, threads):
@@ -287,6 +328,10 @@ def main():
     if rank == 0 and not args.no_fused:
         fused = fused_disparity_phase(B, H, W, 10, dev, stream)
 
+    bf16 = None
+    if rank == 0 and not args.no_bf16:
+        bf16 = bf16_warp_phase(64, 368, 560, 20, dev, stream)
+
     hole = None
     if rank == 0 and not args.no_hole_fill:  # untimed by the driver's clock contract: after the K steps
         rgb, _, hole = hole_fill_phase(out[0], out[1], out[2], args.hole_fill_steps, stream)
@@ -327,6 +372,7 @@ def main():
             "cpu_baseline": cpu,
             "hole_fill": hole,
             "fused_disparity": fused,
+            "bf16_warp": bf16,
         }
         print(json.dumps(rec), flush=True)
     if world > 1:

@@ -17,6 +17,10 @@
  *       alt_cuda.fw.FW.forward(obj, flow, depth)  -- alt_cuda/fw.py:19-59,
  *       batched: the meshgrid add / clamp / int64 truncation of fw.py:27-42 is
  *       done inside the kernel, the add in the flow's dtype (fw.py:31).
+ *   ofd_fw_forward_warp_flow_bf16
+ *       no reference counterpart (FW is float32-only, fw.py:40-43, and
+ *       AT_DISPATCH_FLOATING_TYPES excludes bf16): the on-the-fly training-loop
+ *       warp of SURVEY.md 8(d) config 5 / 8(f) rank 4, bf16 obj and output.
  *   ofd_fw_warp_disparity_f32 / _f64depth
  *       preprocess.py:356-359 (Convert.depth_to_disparity, disparity_to_flow,
  *       the obj concatenation and the FW call) fused into one warp: the flow
@@ -124,6 +128,17 @@ int ofd_fw_forward_warp_flow_f64flow(const float *obj, const double *flow, const
                                      float *output, float *valid, float *collision,
                                      int64_t B, int64_t C, int64_t H, int64_t W,
                                      void *workspace, size_t workspace_bytes, void *stream);
+
+/* FW.forward on bf16 planes (raw bf16 bit patterns as uint16_t): obj and
+ * output [B,C,H,W] bf16; flow [B,2,H,W], depth, valid, collision [B,1,H,W]
+ * f32, the z-test and the coordinate arithmetic exactly as the f32 entry.
+ * The warp only selects source values, so output == the f32 entry's output on
+ * the same (bf16-valued) obj, bit for bit.  TILE engine only: requires
+ * C*H*W < 2^30 (OFD_FW_ETOOBIG); obj / output 2-byte aligned. */
+int ofd_fw_forward_warp_flow_bf16(const uint16_t *obj, const float *flow, const float *depth,
+                                  uint16_t *output, float *valid, float *collision,
+                                  int64_t B, int64_t C, int64_t H, int64_t W,
+                                  void *workspace, size_t workspace_bytes, void *stream);
 
 /* Fused depth -> disparity -> flow -> FW: preprocess.py:356-359,
  *     disp0   = Convert.depth_to_disparity(depth)         (s * 50 * 1 / depth, :239-246)

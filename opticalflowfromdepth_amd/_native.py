@@ -39,6 +39,7 @@ SIGNATURES = {
     "ofd_fw_forward_warping_f64": ([_P] * 7 + [_I64] * 4 + [_P, _SZ, _P], ctypes.c_int),
     "ofd_fw_forward_warp_flow_f32": ([_P] * 6 + [_I64] * 4 + [_P, _SZ, _P], ctypes.c_int),
     "ofd_fw_forward_warp_flow_f64flow": ([_P] * 6 + [_I64] * 4 + [_P, _SZ, _P], ctypes.c_int),
+    "ofd_fw_forward_warp_flow_bf16": ([_P] * 6 + [_I64] * 4 + [_P, _SZ, _P], ctypes.c_int),
     "ofd_fw_warp_disparity_f32": ([_P, _I64, _P, _P, _P, _P, _P] + [_I64] * 3 + [_P, _SZ, _P], ctypes.c_int),
     "ofd_fw_warp_disparity_f64depth": ([_P, _I64, _P, _P, _P, _P, _P] + [_I64] * 3 + [_P, _SZ, _P], ctypes.c_int),
     "ofd_inpaint_workspace_bytes": ([_I64, _I64, _I64], _SZ),

@@ -569,8 +569,8 @@ __device__ __forceinline__ void band_major_tile(unsigned lin, int nimg, const Ti
 // planes, gathered from obj right out of the LDS z-buffer.
 struct SplatIO {
     float *valid, *coll;
-    const float *obj;  // kFuse only: [B][Cobj][H][W]
-    float *out;        // kFuse only: [B][C][H][W]
+    const void *obj;   // kFuse only: [B][Cobj][H][W] of the element type E (float, or bf16 bits)
+    void *out;         // kFuse only: [B][C][H][W], E
     int C;             // output channels
     int Cobj, gen_at;  // obj channels; output channel of the first of Coords::kGen generated ones
 };
@@ -587,7 +587,7 @@ struct SplatCfg {
 // One target tile (linear index `lin` of the chunk's band-major tile order).
 // Every barrier is LDS-only: global loads are consumed by the thread that
 // issued them, and the published stores are never waited for.
-template <typename Coords, bool kVec, bool kFuse, bool kStamp, typename Cfg>
+template <typename Coords, bool kVec, bool kFuse, bool kStamp, typename Cfg, typename E = float>
 __device__ __forceinline__ void splat_tile(TileLds &L, unsigned lin, const Coords &co, const float *__restrict__ depth,
                                            const SplatIO &io, const ChunkArgs &a, int H, int W, int64_t HW,
                                            const TileGeom &g, unsigned long long *stamps) {
@@ -745,17 +745,24 @@ __device__ __forceinline__ void splat_tile(TileLds &L, unsigned lin, const Coord
         // valid, collision, and the winners' C channels: kT targets per thread
         // with all their gathers in flight before any store.  The output
         // planes and masks are touched once: non-temporal.
+        // E = unsigned short: bf16 planes moved as raw bits (the warp only
+        // selects a source value, so no rounding happens anywhere)
+        static_assert(std::is_same<E, float>::value || Coords::kGen == 0, "generated channels are float32");
         constexpr int kT = Cfg::kGT, kCh = 8;
         const int C = io.C;
-        const float *ob = io.obj + b * int64_t(io.Cobj) * HW;
-        float *oo = io.out + b * int64_t(C) * HW;
+        const E *ob = static_cast<const E *>(io.obj) + b * int64_t(io.Cobj) * HW;
+        E *oo = static_cast<E *>(io.out) + b * int64_t(C) * HW;
         const unsigned uHW = unsigned(HW);
-        auto source = [&](int c, unsigned wi) -> float {
-            if (Coords::kGen == 0 || c < io.gen_at) return ob[unsigned(c) * uHW + wi];
-            float g[3];
-            co.gen_all(b, wi, g);
-            if (c < io.gen_at + Coords::kGen) return c == io.gen_at ? g[0] : (c == io.gen_at + 1 ? g[1] : g[2]);
-            return ob[unsigned(c - Coords::kGen) * uHW + wi];
+        auto source = [&](int c, unsigned wi) -> E {
+            if constexpr (Coords::kGen == 0) {
+                return ob[unsigned(c) * uHW + wi];
+            } else {
+                if (c < io.gen_at) return ob[unsigned(c) * uHW + wi];
+                float g[3];
+                co.gen_all(b, wi, g);
+                if (c < io.gen_at + Coords::kGen) return c == io.gen_at ? g[0] : (c == io.gen_at + 1 ? g[1] : g[2]);
+                return ob[unsigned(c - Coords::kGen) * uHW + wi];
+            }
         };
 #pragma unroll
         for (int k = 0; k < TW * TH / Cfg::kThr; k += kT) {
@@ -780,12 +787,12 @@ __device__ __forceinline__ void splat_tile(TileLds &L, unsigned lin, const Coord
             // channels generated from the winner (Coords::kGen of them at output
             // channel gen_at; obj supplies the others): one source read per target
             for (int c0 = 0; c0 < C; c0 += kCh) {
-                float o[kT][kCh];
+                E o[kT][kCh];
 #pragma unroll
                 for (int u = 0; u < kT; ++u)
 #pragma unroll
                     for (int cc = 0; cc < kCh; ++cc)
-                        o[u][cc] = (w[u] != WIN_NONE && c0 + cc < C) ? source(c0 + cc, w[u]) : 0.f;
+                        o[u][cc] = (w[u] != WIN_NONE && c0 + cc < C) ? source(c0 + cc, w[u]) : E(0);
 #pragma unroll
                 for (int u = 0; u < kT; ++u)
 #pragma unroll
@@ -856,7 +863,8 @@ __global__ __launch_bounds__(Cfg::kThr, Cfg::kMinW) void splat_kernel(Coords co,
 // the last workgroup out restores them, so the next launch starts clean.
 // Placement and order affect speed only: every tile is processed exactly
 // once, and no workgroup ever waits for another.
-template <typename Coords, bool kVec, bool kFuse = true, bool kStamp = false, typename Cfg = FusedCfg>
+template <typename Coords, bool kVec, bool kFuse = true, bool kStamp = false, typename Cfg = FusedCfg,
+          typename E = float>
 __global__ __launch_bounds__(Cfg::kThr, Cfg::kMinW) void splat_persist_kernel(Coords co, const float *__restrict__ depth,
                                                                         SplatIO io, ChunkArgs a, int H, int W,
                                                                         int64_t HW, TileGeom g,
@@ -887,7 +895,7 @@ __global__ __launch_bounds__(Cfg::kThr, Cfg::kMinW) void splat_persist_kernel(Co
         lds_barrier();
         const unsigned lin = L.next;
         if (lin == ~0u) return;
-        splat_tile<Coords, kVec, kFuse, kStamp, Cfg>(L, lin, co, depth, io, a, H, W, HW, g, stamps);
+        splat_tile<Coords, kVec, kFuse, kStamp, Cfg, E>(L, lin, co, depth, io, a, H, W, HW, g, stamps);
         // splat_tile ends with LDS reads of the z-buffer; the next iteration's
         // barrier orders them before the next tile's initialisation
     }
@@ -1131,9 +1139,9 @@ unsigned resident_slots(K kernel, int threads) {
     return unsigned(cus) * unsigned(per);
 }
 
-template <typename Coords, bool kVec, typename Cfg = FusedCfgFor<Coords>>
+template <typename Coords, bool kVec, typename Cfg = FusedCfgFor<Coords>, typename E = float>
 unsigned persist_grid(unsigned tiles) {
-    static const unsigned slots = resident_slots(splat_persist_kernel<Coords, kVec, true, false, Cfg>, Cfg::kThr);
+    static const unsigned slots = resident_slots(splat_persist_kernel<Coords, kVec, true, false, Cfg, E>, Cfg::kThr);
     return tiles < slots ? tiles : slots;
 }
 
@@ -1143,10 +1151,14 @@ unsigned persist_grid(unsigned tiles) {
 // HIP events on the stream it runs on.
 hipEvent_t g_prof_start = nullptr, g_prof_stop = nullptr;
 
-template <typename Coords>
-int run_f32(Coords co, const float *obj, const float *depth, float *out, float *valid, float *coll,
+// E: the obj / output element type -- float, or unsigned short for bf16
+// planes (fused TILE engine only, like coordinate sources that generate
+// channels).
+template <typename Coords, typename E = float>
+int run_f32(Coords co, const E *obj, const float *depth, E *out, float *valid, float *coll,
             int64_t B, int64_t C, int64_t H, int64_t W, void *ws, size_t ws_bytes, hipStream_t st,
             int gen_at = -1) {
+    constexpr bool kTileOnly = Coords::kGen > 0 || !std::is_same<E, float>::value;
     const int64_t HW = H * W;
     if (gen_at < 0) gen_at = int(C);
     if (B == 0 || HW == 0) return OFD_FW_OK;
@@ -1157,8 +1169,8 @@ int run_f32(Coords co, const float *obj, const float *depth, float *out, float *
     // the tile engine's gathers use 32-bit offsets inside one image
     // Coordinate sources that generate obj channels run on the fused TILE
     // engine only (the gather is where the channels are generated).
-    if (Coords::kGen > 0 && C * HW >= (int64_t(1) << 30)) return OFD_FW_ETOOBIG;
-    const Mode mode = Coords::kGen > 0 ? Mode::Tile : (C * HW < (int64_t(1) << 30)) ? engine_mode() : Mode::Atomic;
+    if (kTileOnly && C * HW >= (int64_t(1) << 30)) return OFD_FW_ETOOBIG;
+    const Mode mode = kTileOnly ? Mode::Tile : (C * HW < (int64_t(1) << 30)) ? engine_mode() : Mode::Atomic;
 
     // One slab of G images, shared by both engines (so the all-ones key /
     // flag regions are the same bytes whichever engine ran last).  Chunks are
@@ -1180,14 +1192,18 @@ int run_f32(Coords co, const float *obj, const float *depth, float *out, float *
         const int64_t b0 = c * G;
         const int64_t nb = (B - b0) < G ? (B - b0) : G;
         const int64_t px = nb * HW;
-        if (mode == Mode::Atomic) {
-            hipLaunchKernelGGL((splat_atomic_kernel<Coords>), dim3(grid_for(px, kBlock * 4)), dim3(kBlock), 0, st,
-                               co, depth, slab.keys, int(H), int(W), HW, b0, px);
-            if (c == 0 && g_prof_start) (void)hipEventRecord(g_prof_start, st);
-            hipLaunchKernelGGL(resolve_atomic_kernel, dim3(grid_for(px, kBlock * 4)), dim3(kBlock), 0, st,
-                               obj, slab.keys, out, valid, coll, int(C), HW, b0, px);
-            if (c == nch - 1 && g_prof_stop) (void)hipEventRecord(g_prof_stop, st);
-        } else {
+        if constexpr (!kTileOnly) {
+            if (mode == Mode::Atomic) {
+                hipLaunchKernelGGL((splat_atomic_kernel<Coords>), dim3(grid_for(px, kBlock * 4)), dim3(kBlock), 0,
+                                   st, co, depth, slab.keys, int(H), int(W), HW, b0, px);
+                if (c == 0 && g_prof_start) (void)hipEventRecord(g_prof_start, st);
+                hipLaunchKernelGGL(resolve_atomic_kernel, dim3(grid_for(px, kBlock * 4)), dim3(kBlock), 0, st,
+                                   obj, slab.keys, out, valid, coll, int(C), HW, b0, px);
+                if (c == nch - 1 && g_prof_stop) (void)hipEventRecord(g_prof_stop, st);
+                continue;
+            }
+        }
+        {
             const ChunkArgs a{slab, b0, int(nb)};
             const SplatIO io{valid, coll, obj, out, int(C), int(C) - Coords::kGen, gen_at};
             const dim3 bgrid(grid_for(nb * g.nseg, kWaves * kBinSPW));
@@ -1204,16 +1220,17 @@ int run_f32(Coords co, const float *obj, const float *depth, float *out, float *
                 if (c == 0 && g_prof_start) (void)hipEventRecord(g_prof_start, st);
                 using Cfg = FusedCfgFor<Coords>;
                 if (vec)
-                    hipLaunchKernelGGL((splat_persist_kernel<Coords, true, true, false, Cfg>),
-                                       dim3(persist_grid<Coords, true>(tiles)), dim3(Cfg::kThr), 0, st, co, depth, io,
+                    hipLaunchKernelGGL((splat_persist_kernel<Coords, true, true, false, Cfg, E>),
+                                       dim3(persist_grid<Coords, true, Cfg, E>(tiles)), dim3(Cfg::kThr), 0, st, co, depth, io,
                                        a, int(H), int(W), HW, g, nullptr);
                 else
-                    hipLaunchKernelGGL((splat_persist_kernel<Coords, false, true, false, Cfg>),
-                                       dim3(persist_grid<Coords, false>(tiles)), dim3(Cfg::kThr), 0, st, co, depth, io,
+                    hipLaunchKernelGGL((splat_persist_kernel<Coords, false, true, false, Cfg, E>),
+                                       dim3(persist_grid<Coords, false, Cfg, E>(tiles)), dim3(Cfg::kThr), 0, st, co, depth, io,
                                        a, int(H), int(W), HW, g, nullptr);
                 if (c == nch - 1 && g_prof_stop) (void)hipEventRecord(g_prof_stop, st);
                 continue;
             }
+            if constexpr (!kTileOnly) {
             if (vec)
                 hipLaunchKernelGGL((splat_kernel<Coords, true>), sgrid, dim3(kWarpThreads), 0, st, co, depth, io, a,
                                    int(H), int(W), HW, g, nullptr);
@@ -1231,6 +1248,7 @@ int run_f32(Coords co, const float *obj, const float *depth, float *out, float *
                 hipLaunchKernelGGL((resolve2d_kernel<4, kResolveRows, kResolveWX, true, true>), rgrid, rblock, 0, st,
                                    obj, slab.winner, out, int(C), int(H), int(W), HW, b0);
             if (c == nch - 1 && g_prof_stop) (void)hipEventRecord(g_prof_stop, st);
+            }
         }
     }
     const hipError_t e = hipGetLastError();
@@ -1321,6 +1339,19 @@ int ofd_fw_forward_warp_flow_f64flow(const float *obj, const double *flow, const
     FlowCoords<double> co{flow, H * W};
     return run_f32(co, obj, depth, output, valid, collision, B, C, H, W, workspace, workspace_bytes,
                    static_cast<hipStream_t>(stream));
+}
+
+int ofd_fw_forward_warp_flow_bf16(const uint16_t *obj, const float *flow, const float *depth, uint16_t *output,
+                                  float *valid, float *collision, int64_t B, int64_t C, int64_t H, int64_t W,
+                                  void *workspace, size_t workspace_bytes, void *stream) {
+    if (int rc = check_dims(B, C, H, W)) return rc;
+    if (B * H * W > 0 && (!flow || !depth || !valid || !collision || (C > 0 && (!obj || !output))))
+        return OFD_FW_EINVAL;
+    if ((C > 0 && (!aligned(obj, 2) || !aligned(output, 2)))) return OFD_FW_EALIGN;
+    FlowCoords<float> co{flow, H * W};
+    return run_f32<FlowCoords<float>, unsigned short>(
+        co, reinterpret_cast<const unsigned short *>(obj), depth, reinterpret_cast<unsigned short *>(output), valid,
+        collision, B, C, H, W, workspace, workspace_bytes, static_cast<hipStream_t>(stream));
 }
 
 int ofd_fw_warp_disparity_f32(const float *obj, int64_t Cobj, const float *depth, const float *s, float *output,

@@ -24,7 +24,7 @@ import torch
 
 from . import _native
 
-_F32, _F64 = torch.float32, torch.float64
+_F32, _F64, _BF16 = torch.float32, torch.float64, torch.bfloat16
 
 # Reusable key workspaces, one per (device, stream); each call leaves its
 # workspace in the initial all-ones state (see include/ofd_fw.h).
@@ -112,6 +112,11 @@ def forward_warp_flow(obj: torch.Tensor, flow: torch.Tensor, depth: torch.Tensor
     u, channel 1 = y / v), depth [B,1,H,W] float32, all contiguous on one
     device.  Target = trunc(clamp(p0 + flow)) with the add in the flow's dtype.
     ``out`` optionally supplies preallocated (output, valid, collision).
+
+    A bfloat16 obj (with a float32 flow) selects the training-loop variant
+    (no reference counterpart): output in bfloat16,
+    valid / collision float32, the same winners as the float32 op, so the
+    output equals the float32 op's on ``obj.float()`` rounded back to bf16.
     """
     for x, n in ((obj, "obj"), (flow, "flow"), (depth, "depth")):
         _check_input(x, n)
@@ -122,10 +127,13 @@ def forward_warp_flow(obj: torch.Tensor, flow: torch.Tensor, depth: torch.Tensor
         raise RuntimeError(f"flow must have shape {(B, 2, H, W)}, got {tuple(flow.shape)}")
     if tuple(depth.shape) != (B, 1, H, W):
         raise RuntimeError(f"depth must have shape {(B, 1, H, W)}, got {tuple(depth.shape)}")
-    if obj.dtype != _F32 or depth.dtype != _F32:
-        raise RuntimeError("forward_warp_flow expects float32 obj and depth")
+    if obj.dtype not in (_F32, _BF16) or depth.dtype != _F32:
+        raise RuntimeError("forward_warp_flow expects a float32 or bfloat16 obj and a float32 depth")
     if flow.dtype not in (_F32, _F64):
         raise RuntimeError(f"flow must be float32 or float64, got {flow.dtype}")
+    bf16 = obj.dtype == _BF16
+    if bf16 and flow.dtype != _F32:
+        raise RuntimeError("the bfloat16 warp takes a float32 flow")
     if flow.device != obj.device or depth.device != obj.device:
         raise RuntimeError("obj, flow and depth must be on one device")
     dev = obj.device
@@ -140,12 +148,14 @@ def forward_warp_flow(obj: torch.Tensor, flow: torch.Tensor, depth: torch.Tensor
             for x, n, shp in ((output, "output", (B, C, H, W)), (valid, "valid", (B, 1, H, W)),
                               (collision, "collision", (B, 1, H, W))):
                 _check_input(x, n)
-                if tuple(x.shape) != shp or x.dtype != _F32 or x.device != dev:
-                    raise RuntimeError(f"out {n} must be float32 {shp} on {dev}")
+                dt = obj.dtype if n == "output" else _F32
+                if tuple(x.shape) != shp or x.dtype != dt or x.device != dev:
+                    raise RuntimeError(f"out {n} must be {dt} {shp} on {dev}")
         nbytes = _ws_bytes(B, H, W, False)
         ws = workspace(dev, nbytes, stream) if nbytes else None
         lib = _native.lib()
-        fn = lib.ofd_fw_forward_warp_flow_f64flow if flow.dtype == _F64 else lib.ofd_fw_forward_warp_flow_f32
+        fn = (lib.ofd_fw_forward_warp_flow_bf16 if bf16 else
+              lib.ofd_fw_forward_warp_flow_f64flow if flow.dtype == _F64 else lib.ofd_fw_forward_warp_flow_f32)
         rc = fn(obj.data_ptr(), flow.data_ptr(), depth.data_ptr(), output.data_ptr(), valid.data_ptr(),
                 collision.data_ptr(), B, C, H, W,
                 ws.data_ptr() if ws is not None else None, ws.numel() if ws is not None else 0,
