@@ -149,6 +149,51 @@ def fused_disparity_phase(B, H, W, steps, dev, stream):
             "parity": "bit-exact vs the unfused FW call and the oracle (tests/test_fused.py)"}
 
 
+def fused_ego_phase(B, H, W, steps, dev, stream):
+    """SURVEY §8f row 1 (ego-motion half): preprocess.py:385-387 as one fused
+    warp (depth -> ego-motion flow -> splat) over B images with float64 depth,
+    next to the unfused sequence (the torch restatement of geometry.py's
+    flow, the concatenation, then forward_warp_flow) and to the one-kernel
+    flow plane (ops.ego_flow).  Algorithmic bytes of the fused call: RGB 12 +
+    depth 8 in, 6 channels 24 + valid 4 + coll 4 out = 52 B/px."""
+    from opticalflowfromdepth_amd import ego_flow, forward_warp_flow, synth, warp_ego
+    seeds = [12345 + i for i in range(B)]
+    depth = synth.normalize_depth(synth.synthetic_depth(seeds, H, W, dev, dtype=torch.float64))
+    rgb = synth.synthetic_rgb(seeds, H, W, dev)
+    T = synth.batch_camera_params(seeds)[1].to(dev)
+    P, ik = synth.projection(H, W, T, dev)
+
+    def unfused():
+        flow = synth.ego_motion_flow(depth, T)
+        d32 = depth.float()
+        return forward_warp_flow(torch.cat((rgb, d32, flow * -1.0), 1), flow, d32)
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        for a, b in ev:
+            a.record(stream)
+            fn()
+            b.record(stream)
+        torch.cuda.synchronize()
+        return sum(a.elapsed_time(b) for a, b in ev) / steps
+
+    ms = timed(lambda: warp_ego(rgb, depth, P, ik))
+    ms_unfused = timed(unfused)
+    ms_flow = timed(lambda: ego_flow(depth, P, ik))
+    ms_flow_torch = timed(lambda: synth.ego_motion_flow(depth, T))
+    px = B * H * W
+    gbs = px * 52 / (ms / 1e3) / 1e9
+    return {"metric": "Mpix/s fused depth->ego-motion flow->splat (preprocess.py:385-387), C=6 out",
+            "value": round(px / (ms / 1e3) / 1e6, 1), "unit": "Mpix/s", "ms_per_step": round(ms, 4),
+            "unfused_ms_per_step": round(ms_unfused, 4), "images": B, "steps": steps,
+            "ego_flow_plane_ms": round(ms_flow, 4), "ego_flow_torch_ms": round(ms_flow_torch, 4),
+            "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(gbs / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_px": 52},
+            "parity": "bit-exact vs FW on ego_flow's plane; flow within 8 ulp of the reference's (tests/test_ego.py)"}
+
+
 def bf16_warp_phase(B, H, W, steps, dev, stream):
     """the training-loop warp on bf16
     planes (no reference counterpart), at 368x560, next to the float32 warp of
@@ -324,9 +369,10 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(obj, flow, depth, args.cpu_seconds, threads)
 
-    fused = None
+    fused = fused_ego = None
     if rank == 0 and not args.no_fused:
         fused = fused_disparity_phase(B, H, W, 10, dev, stream)
+        fused_ego = fused_ego_phase(B, H, W, 10, dev, stream)
 
     bf16 = None
     if rank == 0 and not args.no_bf16:
@@ -372,6 +418,7 @@ def main():
             "cpu_baseline": cpu,
             "hole_fill": hole,
             "fused_disparity": fused,
+            "fused_ego": fused_ego,
             "bf16_warp": bf16,
         }
         print(json.dumps(rec), flush=True)

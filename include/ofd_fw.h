@@ -25,6 +25,13 @@
  *       preprocess.py:356-359 (Convert.depth_to_disparity, disparity_to_flow,
  *       the obj concatenation and the FW call) fused into one warp: the flow
  *       and obj's depth / flow channels are derived from the depth in-kernel.
+ *   ofd_fw_ego_flow_f32 / _f64depth
+ *       Convert.depth_to_random_flow (preprocess.py:265-298) with
+ *       geometry.BackprojectDepth / Project3D (geometry.py:17-67): the
+ *       ego-motion flow plane from depth, inv_K and P = (K @ T)[:3].
+ *   ofd_fw_warp_ego_f32 / _f64depth
+ *       preprocess.py:371-373 / :385-387 (ego-motion flow, the obj
+ *       concatenation and the FW call) fused into one warp.
  *   ofd_fw_workspace_bytes / ofd_fw_workspace_init
  *       no reference counterpart: the reference allocates its z-buffer `dlut`
  *       per call (fw_cuda_kernel.cu:58); here the caller owns a reusable
@@ -162,6 +169,37 @@ int ofd_fw_warp_disparity_f32(const float *obj, int64_t Cobj, const float *depth
 int ofd_fw_warp_disparity_f64depth(const float *obj, int64_t Cobj, const double *depth, const float *s,
                                    float *output, float *valid, float *collision, int64_t B, int64_t H,
                                    int64_t W, void *workspace, size_t workspace_bytes, void *stream);
+
+/* Ego-motion flow plane (preprocess.py:265-298, geometry.py:17-67):
+ *   cam  = float32(depth * inv_K[:3,:3] @ [x, y, 1])
+ *   cp   = P @ [cam, 1]
+ *   pix  = cp[:2] / (cp[2] + 1e-7), normalised to [-1, 1] and back to pixels
+ *   flow = pix - [x, y]
+ * depth [B,1,H,W] f32 or f64 (device); P [B,3,4] f32 (device) = (K @ T)[:, :3]
+ * as Project3D computes it; inv_K: HOST pointer to the 9 floats of
+ * inv_K[:3,:3] (row-major; one camera for the batch, Plausible.K); flow
+ * [B,2,H,W] f32 (device).  The products accumulate with fused multiply-adds
+ * in k order, so the flow equals the reference's to float32 rounding, not bit
+ * for bit (torch's GEMM order is unspecified). */
+int ofd_fw_ego_flow_f32(const float *depth, const float *P, const float *inv_K, float *flow, int64_t B, int64_t H,
+                        int64_t W, void *stream);
+int ofd_fw_ego_flow_f64depth(const double *depth, const float *P, const float *inv_K, float *flow, int64_t B,
+                             int64_t H, int64_t W, void *stream);
+
+/* Fused depth -> ego-motion flow -> FW (preprocess.py:371-373, :385-387):
+ *     flow    = the ofd_fw_ego_flow_* plane
+ *     obj_all = torch.cat((obj[:3], depth, flow * -1.0, obj[3:]))
+ *     FW(obj_all, flow, depth)
+ * with neither the flow nor obj_all stored; arguments as ofd_fw_ego_flow_*
+ * and ofd_fw_warp_disparity_*.  Bit-identical to ofd_fw_forward_warp_flow_f32
+ * on the materialised ofd_fw_ego_flow_* plane (the same device code computes
+ * the flow in both).  TILE engine only: (Cobj+3)*H*W < 2^30. */
+int ofd_fw_warp_ego_f32(const float *obj, int64_t Cobj, const float *depth, const float *P, const float *inv_K,
+                        float *output, float *valid, float *collision, int64_t B, int64_t H, int64_t W,
+                        void *workspace, size_t workspace_bytes, void *stream);
+int ofd_fw_warp_ego_f64depth(const float *obj, int64_t Cobj, const double *depth, const float *P,
+                             const float *inv_K, float *output, float *valid, float *collision, int64_t B, int64_t H,
+                             int64_t W, void *workspace, size_t workspace_bytes, void *stream);
 
 #ifdef __cplusplus
 }

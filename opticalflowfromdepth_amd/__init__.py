@@ -8,10 +8,12 @@ gfx950 behind a C ABI (include/ofd_fw.h), with the reference's Python surface:
 * ``forward_warping``  -- drop-in for the extension op ``fw_cuda.forward_warping``
 * ``forward_warp_flow``-- batched FW core (flow -> splat in one native call)
 * ``warp_disparity``   -- preprocess.py:356-359 fused (depth -> disparity -> flow -> splat)
+* ``warp_ego``         -- preprocess.py:371-373 / :385-387 fused (depth -> ego-motion flow -> splat)
+* ``ego_flow``         -- the ego-motion flow plane (preprocess.py:265-298) in one kernel
 * ``inpaint``          -- batched GPU hole-fill replacing ``utils.inpaint``
 """
 from .fw import FW
-from .ops import forward_warp_flow, forward_warping, inpaint, warp_disparity
+from .ops import ego_flow, forward_warp_flow, forward_warping, inpaint, warp_disparity, warp_ego
 
-__all__ = ["FW", "forward_warping", "forward_warp_flow", "warp_disparity", "inpaint"]
+__all__ = ["FW", "forward_warping", "forward_warp_flow", "warp_disparity", "warp_ego", "ego_flow", "inpaint"]
 __version__ = "0.1.0"

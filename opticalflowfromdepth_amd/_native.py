@@ -42,6 +42,10 @@ SIGNATURES = {
     "ofd_fw_forward_warp_flow_bf16": ([_P] * 6 + [_I64] * 4 + [_P, _SZ, _P], ctypes.c_int),
     "ofd_fw_warp_disparity_f32": ([_P, _I64, _P, _P, _P, _P, _P] + [_I64] * 3 + [_P, _SZ, _P], ctypes.c_int),
     "ofd_fw_warp_disparity_f64depth": ([_P, _I64, _P, _P, _P, _P, _P] + [_I64] * 3 + [_P, _SZ, _P], ctypes.c_int),
+    "ofd_fw_ego_flow_f32": ([_P] * 4 + [_I64] * 3 + [_P], ctypes.c_int),
+    "ofd_fw_ego_flow_f64depth": ([_P] * 4 + [_I64] * 3 + [_P], ctypes.c_int),
+    "ofd_fw_warp_ego_f32": ([_P, _I64] + [_P] * 6 + [_I64] * 3 + [_P, _SZ, _P], ctypes.c_int),
+    "ofd_fw_warp_ego_f64depth": ([_P, _I64] + [_P] * 6 + [_I64] * 3 + [_P, _SZ, _P], ctypes.c_int),
     "ofd_inpaint_workspace_bytes": ([_I64, _I64, _I64], _SZ),
     "ofd_inpaint_telea_f32": ([_P] * 4 + [_I64] * 4 + [ctypes.c_int, _P, _SZ, _P], ctypes.c_int),
 }

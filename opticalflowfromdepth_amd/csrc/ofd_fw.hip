@@ -149,7 +149,7 @@ __device__ __forceinline__ void load4(const T *__restrict__ q, T v[4], int n) {
 // Coordinate sources whose z-test depth is the separate float32 depth plane
 // and that generate no obj channels.
 #define KEY_DEPTH_FROM_PLANE                                                                            \
-    static constexpr int kGen = 0;                                                                    \
+    static constexpr int kGen = 0, kGenGT = 0;                                                        \
     template <bool kVec>                                                                              \
     __device__ __forceinline__ void load4d(int64_t b, int64_t p, V x[4], V y[4], float dk[4], int n,  \
                                            const float *depth) const {                                \
@@ -176,7 +176,7 @@ struct SafeF32 {  // fw_cuda.forward_warping inputs: safe_y, safe_x [B,1,H,W]
         ::load4<kVec>(sy + b * HW + p, y, n);
     }
     __host__ bool vec_ok() const { return (uintptr_t(sx) | uintptr_t(sy)) % 16 == 0; }
-    __device__ __forceinline__ void target(int, int, V x, V y, int H, int W, int &tx, int &ty) const {
+    __device__ __forceinline__ void target(int64_t, int, int, V x, V y, int H, int W, int &tx, int &ty) const {
         target_safe<float>(x, y, H, W, tx, ty);
     }
     KEY_DEPTH_FROM_PLANE
@@ -199,7 +199,7 @@ struct FlowCoords {  // FW.forward input: flow [B,2,H,W], ch0 = x, ch1 = y
         ::load4<kVec>(f + HW, y, n);
     }
     __host__ bool vec_ok() const { return uintptr_t(flow) % 16 == 0; }
-    __device__ __forceinline__ void target(int i, int j, V x, V y, int H, int W, int &tx, int &ty) const {
+    __device__ __forceinline__ void target(int64_t, int i, int j, V x, V y, int H, int W, int &tx, int &ty) const {
         target_flow<F>(i, j, x, y, H, W, tx, ty);
     }
     KEY_DEPTH_FROM_PLANE
@@ -215,7 +215,7 @@ struct FlowCoords {  // FW.forward input: flow [B,2,H,W], ch0 = x, ch1 = y
 template <typename D>
 struct DisparityCoords {
     using V = D;
-    static constexpr int kGen = 3;
+    static constexpr int kGen = 3, kGenGT = 4;
     const D *depth;
     const float *s;  // [B] per-image scale
     int64_t HW;
@@ -257,10 +257,142 @@ struct DisparityCoords {
         g[2] = 0.0f;
     }
     __host__ bool vec_ok() const { return uintptr_t(depth) % 16 == 0; }
-    __device__ __forceinline__ void target(int i, int j, V x, V y, int H, int W, int &tx, int &ty) const {
+    __device__ __forceinline__ void target(int64_t, int i, int j, V x, V y, int H, int W, int &tx, int &ty) const {
         target_flow<D>(i, j, x, y, H, W, tx, ty);
     }
 };
+
+// Ego-motion flow (Convert.depth_to_random_flow, preprocess.py:265-298, with
+// geometry.BackprojectDepth / Project3D, geometry.py:17-67) of the source at
+// pixel (i, j) with depth d, in the reference's operation order:
+//   cam   = inv_K[:3,:3] @ [i, j, 1]                      (geometry.py:38)
+//   cam   = float32(d * cam)  (in d's dtype)              (:39-40)
+//   cp    = P @ [cam, 1],  P = (K @ T)[:3]                (:57-59)
+//   pix   = cp[:2] / (cp[2] + 1e-7)                       (:61)
+//   pix   = (pix / (size - 1) - 0.5) * 2                  (:64-66)
+//   p1    = (pix + 1) / 2 * (size - 1);  flow = p1 - p0   (preprocess.py:284-291)
+// The two small matrix products accumulate k = 0, 1, ... with fused
+// multiply-adds, as a GEMM inner loop does; torch's own GEMM order is not
+// specified, so the flow matches the reference to float32 rounding (not
+// bit-exact; tests/test_ego.py).  Every use of this function -- the flow
+// plane kernel, BIN, SPLAT and the generated channels -- runs the same code,
+// so the fused warp is bit-identical to FW on ofd_fw_ego_flow's plane.
+struct EgoCam {
+    float ik[9];  // inv_K[:3,:3], row-major (the same for every image)
+};
+
+template <typename D>
+__device__ __forceinline__ void ego_flow_at(const EgoCam &cam, const float *__restrict__ Pb, int i, int j, D d,
+                                            int H, int W, float &fx, float &fy) {
+    const float x = float(i), y = float(j);
+    float c[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) c[k] = fmaf(cam.ik[3 * k + 2], 1.0f, fmaf(cam.ik[3 * k + 1], y, cam.ik[3 * k] * x));
+    float X[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) X[k] = float(d * D(c[k]));
+    float cp[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+        cp[k] = fmaf(Pb[4 * k + 3], 1.0f, fmaf(Pb[4 * k + 2], X[2], fmaf(Pb[4 * k + 1], X[1], Pb[4 * k] * X[0])));
+    const float den = cp[2] + 1e-7f;
+    float u = cp[0] / den, v = cp[1] / den;
+    u = u / float(W - 1);
+    v = v / float(H - 1);
+    u = (u - 0.5f) * 2.0f;
+    v = (v - 0.5f) * 2.0f;
+    u = (u + 1.0f) / 2.0f;
+    v = (v + 1.0f) / 2.0f;
+    u = u * float(W - 1);
+    v = v * float(H - 1);
+    fx = u - x;
+    fy = v - y;
+}
+
+// Fused depth -> ego-motion flow -> splat: the flow is derived from the depth
+// (and the image's P) in BIN and SPLAT, and SPLAT generates obj's channels
+// depth, flow * -1.0 (x, y) from the winner (preprocess.py:371-373, :385-386).
+template <typename D>
+struct EgoCoords {
+    // The coordinate registers carry the source's depth (x; y is unused):
+    // the flow is computed in target(), after every load of a batch of
+    // sources has been issued, which keeps SPLAT's loads in flight together.
+    using V = D;
+    static constexpr int kGen = 3, kGenGT = 2;
+    const D *depth;
+    const float *P;  // [B][3][4] float32 (K @ T)[:3]
+    EgoCam cam;
+    int64_t HW;
+    int H, W;
+    // b is wave-uniform at every call site (BIN: one segment per wave; SPLAT:
+    // one image per tile): the image's P is read through the scalar cache
+    __device__ __forceinline__ const float *Pof(int64_t b) const {
+        return P + 12 * int64_t(__builtin_amdgcn_readfirstlane(int(b)));
+    }
+    template <bool kVec>
+    __device__ __forceinline__ void load4d(int64_t b, int64_t p, V x[4], V y[4], float dk[4], int n,
+                                           const float *) const {
+        ::load4<kVec>(depth + b * HW + p, x, n);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            y[e] = D(0);
+            dk[e] = float(x[e]);
+        }
+    }
+    template <bool kVec>
+    __device__ __forceinline__ void load4(int64_t b, int64_t p, V x[4], V y[4], int n) const {
+        ::load4<kVec>(depth + b * HW + p, x, n);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) y[e] = D(0);
+    }
+    __device__ __forceinline__ void load(int64_t b, int64_t p, V &x, V &y) const {
+        x = depth[b * HW + p];
+        y = D(0);
+    }
+    __device__ __forceinline__ float key_depth(int64_t b, int64_t p, const float *) const {
+        return float(depth[b * HW + p]);
+    }
+    // generated obj channels of source w: depth, flow_x * -1.0, flow_y * -1.0
+    __device__ __forceinline__ void gen_all(int64_t b, unsigned w, float g[3]) const {
+        const D d = depth[b * HW + w];
+        const unsigned j = w / unsigned(W), i = w - j * unsigned(W);
+        float fx, fy;
+        ego_flow_at<D>(cam, Pof(b), int(i), int(j), d, H, W, fx, fy);
+        g[0] = float(d);
+        g[1] = fx * -1.0f;
+        g[2] = fy * -1.0f;
+    }
+    __host__ bool vec_ok() const { return uintptr_t(depth) % 16 == 0; }
+    __device__ __forceinline__ void target(int64_t b, int i, int j, V d, V, int H_, int W_, int &tx,
+                                           int &ty) const {
+        float fx, fy;
+        ego_flow_at<D>(cam, Pof(b), i, j, d, H, W, fx, fy);
+        target_flow<float>(i, j, fx, fy, H_, W_, tx, ty);
+    }
+};
+
+// The ego-motion flow plane itself ([B,2,H,W] float32), four pixels of a row
+// per thread.
+template <typename D>
+__global__ __launch_bounds__(256) void ego_flow_kernel(EgoCoords<D> co, float *__restrict__ flow, int64_t B) {
+    const int64_t q = int64_t(blockIdx.x) * 256 + threadIdx.x;  // quad index over [B][H][ceil(W/4)]
+    const int64_t qpr = (co.W + 3) / 4;
+    const int64_t row = q / qpr;
+    if (row >= B * co.H) return;
+    const int64_t b = row / co.H;
+    const int j = int(row - b * co.H), i0 = int(q - row * qpr) * 4;
+    const float *Pb = co.P + 12 * b;
+    float *fxp = flow + b * 2 * co.HW + int64_t(j) * co.W, *fyp = fxp + co.HW;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int i = i0 + e;
+        if (i >= co.W) break;
+        float fx, fy;
+        ego_flow_at<D>(co.cam, Pb, i, j, co.depth[b * co.HW + int64_t(j) * co.W + i], co.H, co.W, fx, fy);
+        fxp[i] = fx;
+        fyp[i] = fy;
+    }
+}
 
 // ---------------------------------------------------------------- wave helpers
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
@@ -447,7 +579,7 @@ __device__ __forceinline__ void bin_segment(const Coords &co, const float *__res
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             tx[q][e] = ty[q][e] = -1;
-            if (i0 + e < W && j < H) co.target(i0 + e, j, x[q][e], y[q][e], H, W, tx[q][e], ty[q][e]);
+            if (i0 + e < W && j < H) co.target(b, i0 + e, j, x[q][e], y[q][e], H, W, tx[q][e], ty[q][e]);
         }
     }
     // per lane: packed (tile x, tile y) min and (0xFFFF - tile x, 0xFFFF - tile y) min
@@ -709,7 +841,7 @@ __device__ __forceinline__ void splat_tile(TileLds &L, unsigned lin, const Coord
                     const int i = ii[u] + q, j = jj[u];
                     if (i >= W) break;
                     int tx, ty;
-                    co.target(i, j, cx[u][q], cy[u][q], H, W, tx, ty);
+                    co.target(b, i, j, cx[u][q], cy[u][q], H, W, tx, ty);
                     const int lx = tx - x0, ly = ty - y0;
                     if (tx >= 0 && unsigned(lx) < unsigned(TW) && unsigned(ly) < unsigned(TH))
                         atomicMin(&L.zk[ly * TW + lx], make_key(d[u][q], unsigned(j * W + i)));
@@ -839,9 +971,12 @@ using SplitCfg = SplatCfg<512, 2, 8>;  // split engine: 4 workgroups / CU, light
 using FusedCfg = SplatCfg<512, 8, 4>;
 // coordinate sources that generate channels carry the generated values and a
 // division per source: 4 targets in flight keeps them inside 128 VGPRs
-using FusedGenCfg = SplatCfg<512, 4, 4>;
+// (Coords::kGenGT of them: 4 for the disparity source, 2 for the ego-motion
+// source, whose per-target projection is the heavier)
 template <typename Coords>
-using FusedCfgFor = typename std::conditional<Coords::kGen == 0, FusedCfg, FusedGenCfg>::type;
+using FusedGenCfg = SplatCfg<512, Coords::kGenGT, 4>;
+template <typename Coords>
+using FusedCfgFor = typename std::conditional<Coords::kGen == 0, FusedCfg, FusedGenCfg<Coords>>::type;
 
 template <typename Coords, bool kVec, bool kFuse = false, bool kStamp = false, typename Cfg = SplitCfg>
 __global__ __launch_bounds__(Cfg::kThr, Cfg::kMinW) void splat_kernel(Coords co, const float *__restrict__ depth,
@@ -964,7 +1099,7 @@ __global__ __launch_bounds__(kBlock) void splat_atomic_kernel(Coords co, const f
             typename Coords::V x, y;
             co.load(b, p, x, y);
             int tx, ty;
-            co.target(i, j, x, y, H, W, tx, ty);
+            co.target(b, i, j, x, y, H, W, tx, ty);
             if (tx >= 0) {
                 t = int(bl * HW) + ty * W + tx;  // chunk-local slot (chunk_px < 2^31)
                 key = make_key(co.key_depth(b, p, depth), unsigned(p));
@@ -1379,6 +1514,67 @@ int ofd_fw_warp_disparity_f64depth(const float *obj, int64_t Cobj, const double 
     DisparityCoords<double> co{depth, s, H * W};
     return run_f32(co, obj, nullptr, output, valid, collision, B, C, H, W, workspace, workspace_bytes,
                    static_cast<hipStream_t>(stream), int(Cobj < 3 ? Cobj : 3));
+}
+
+}  // extern "C"
+
+namespace {
+template <typename D>
+int ego_flow(const D *depth, const float *P, const float *inv_K, float *flow, int64_t B, int64_t H, int64_t W,
+             void *stream) {
+    if (int rc = check_dims(B, 1, H, W)) return rc;
+    if (B * H * W == 0) return OFD_FW_OK;
+    if (!depth || !P || !inv_K || !flow) return OFD_FW_EINVAL;
+    if (!aligned(depth, sizeof(D)) || !aligned(P, 4) || !aligned(flow, 4)) return OFD_FW_EALIGN;
+    EgoCoords<D> co{depth, P, {}, H * W, int(H), int(W)};
+    for (int k = 0; k < 9; ++k) co.cam.ik[k] = inv_K[k];
+    const int64_t quads = B * H * ((W + 3) / 4);
+    hipLaunchKernelGGL((ego_flow_kernel<D>), dim3(grid_for(quads)), dim3(kBlock), 0, static_cast<hipStream_t>(stream),
+                       co, flow, B);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? OFD_FW_OK : int(e);
+}
+
+template <typename D>
+int warp_ego(const float *obj, int64_t Cobj, const D *depth, const float *P, const float *inv_K, float *output,
+             float *valid, float *collision, int64_t B, int64_t H, int64_t W, void *workspace, size_t workspace_bytes,
+             void *stream) {
+    if (Cobj < 0) return OFD_FW_EINVAL;
+    const int64_t C = Cobj + 3;
+    if (int rc = check_dims(B, C, H, W)) return rc;
+    if (B * H * W > 0 && (!depth || !P || !inv_K || !valid || !collision || !output || (Cobj > 0 && !obj)))
+        return OFD_FW_EINVAL;
+    if (!aligned(depth, sizeof(D))) return OFD_FW_EALIGN;
+    EgoCoords<D> co{depth, P, {}, H * W, int(H), int(W)};
+    if (inv_K)
+        for (int k = 0; k < 9; ++k) co.cam.ik[k] = inv_K[k];
+    return run_f32(co, obj, nullptr, output, valid, collision, B, C, H, W, workspace, workspace_bytes,
+                   static_cast<hipStream_t>(stream), int(Cobj < 3 ? Cobj : 3));
+}
+}  // namespace
+
+extern "C" {
+
+int ofd_fw_ego_flow_f32(const float *depth, const float *P, const float *inv_K, float *flow, int64_t B, int64_t H,
+                        int64_t W, void *stream) {
+    return ego_flow(depth, P, inv_K, flow, B, H, W, stream);
+}
+
+int ofd_fw_ego_flow_f64depth(const double *depth, const float *P, const float *inv_K, float *flow, int64_t B,
+                             int64_t H, int64_t W, void *stream) {
+    return ego_flow(depth, P, inv_K, flow, B, H, W, stream);
+}
+
+int ofd_fw_warp_ego_f32(const float *obj, int64_t Cobj, const float *depth, const float *P, const float *inv_K,
+                        float *output, float *valid, float *collision, int64_t B, int64_t H, int64_t W,
+                        void *workspace, size_t workspace_bytes, void *stream) {
+    return warp_ego(obj, Cobj, depth, P, inv_K, output, valid, collision, B, H, W, workspace, workspace_bytes, stream);
+}
+
+int ofd_fw_warp_ego_f64depth(const float *obj, int64_t Cobj, const double *depth, const float *P,
+                             const float *inv_K, float *output, float *valid, float *collision, int64_t B, int64_t H,
+                             int64_t W, void *workspace, size_t workspace_bytes, void *stream) {
+    return warp_ego(obj, Cobj, depth, P, inv_K, output, valid, collision, B, H, W, workspace, workspace_bytes, stream);
 }
 
 int ofd_fw_forward_warping_f64(const double *obj, const double *safe_y, const double *safe_x,

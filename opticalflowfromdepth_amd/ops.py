@@ -8,6 +8,10 @@ meaning, same checks and messages, same outputs, for any batch size B.
 ``forward_warp_flow`` is the batched FW.forward path (alt_cuda/fw.py:19-59)
 with the coordinate arithmetic fused into the splat kernel.
 
+``warp_disparity`` / ``warp_ego`` fuse the first stage's flow synthesis into
+the warp (preprocess.py:356-359 / :371-373, :385-387); ``ego_flow`` is the
+ego-motion flow plane alone (preprocess.py:265-298).
+
 ``inpaint`` is the batched hole-fill that replaces ``utils.inpaint``
 (utils.py:136-151) with the layered Telea kernels of csrc/ofd_inpaint.hip.
 
@@ -261,4 +265,83 @@ def warp_disparity(obj: torch.Tensor, depth: torch.Tensor, s: torch.Tensor,
                 collision.data_ptr(), B, H, W, ws.data_ptr() if ws is not None else None,
                 ws.numel() if ws is not None else 0, stream.cuda_stream)
         _native.check(rc, "warp_disparity")
+    return output, valid, collision
+
+
+def _ego_camera(B, P, inv_K, dev):
+    P = torch.as_tensor(P, dtype=_F32).to(dev).contiguous()
+    if tuple(P.shape) != (B, 3, 4):
+        raise RuntimeError(f"P must have shape {(B, 3, 4)}, got {tuple(P.shape)}")
+    ik = torch.as_tensor(inv_K, dtype=_F32).cpu().contiguous()
+    if tuple(ik.shape) != (3, 3):
+        raise RuntimeError(f"inv_K must be [3,3] (inv_K[:3,:3]), got {tuple(ik.shape)}")
+    return P, ik
+
+
+def ego_flow(depth: torch.Tensor, P: torch.Tensor, inv_K: torch.Tensor) -> torch.Tensor:
+    """Convert.depth_to_random_flow's flow (preprocess.py:265-298, geometry.py:17-67)
+    for a batch: depth [B,1,H,W] float32 / float64, P [B,3,4] = (K @ T)[:, :3]
+    (synth.projection), inv_K [3,3] -> flow [B,2,H,W] float32, equal to the
+    reference's to float32 rounding (include/ofd_fw.h ofd_fw_ego_flow_*)."""
+    _check_input(depth, "depth")
+    if depth.dim() != 4 or depth.shape[1] != 1:
+        raise RuntimeError(f"depth must be [B,1,H,W], got {tuple(depth.shape)}")
+    if depth.dtype not in (_F32, _F64):
+        raise RuntimeError(f"depth must be float32 or float64, got {depth.dtype}")
+    B, _, H, W = depth.shape
+    dev = depth.device
+    P, ik = _ego_camera(B, P, inv_K, dev)
+    with torch.cuda.device(dev):
+        stream = torch.cuda.current_stream(dev)
+        flow = torch.empty(B, 2, H, W, dtype=_F32, device=dev)
+        lib = _native.lib()
+        fn = lib.ofd_fw_ego_flow_f64depth if depth.dtype == _F64 else lib.ofd_fw_ego_flow_f32
+        rc = fn(depth.data_ptr(), P.data_ptr(), ik.data_ptr(), flow.data_ptr(), B, H, W, stream.cuda_stream)
+        _native.check(rc, "ego_flow")
+    return flow
+
+
+def warp_ego(obj: torch.Tensor, depth: torch.Tensor, P: torch.Tensor, inv_K: torch.Tensor,
+             out: Tuple[torch.Tensor, torch.Tensor, torch.Tensor] = None
+             ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """preprocess.py:371-373 / :385-387 fused (include/ofd_fw.h ofd_fw_warp_ego_*):
+
+        flow = ego_flow(depth, P, inv_K)
+        FW(torch.cat((obj[:, :3], depth, flow * -1.0, obj[:, 3:]), 1), flow, depth)
+
+    in one native call that never stores the flow or the concatenation;
+    bit-identical to forward_warp_flow on ``ego_flow``'s plane.  obj
+    [B,Cobj,H,W] float32, depth [B,1,H,W] float32 / float64.  Returns
+    (output [B,Cobj+3,H,W], valid, collision)."""
+    for x, n in ((obj, "obj"), (depth, "depth")):
+        _check_input(x, n)
+    if obj.dim() != 4 or depth.dim() != 4:
+        raise RuntimeError("warp_ego expects obj [B,C,H,W] and depth [B,1,H,W]")
+    B, Cobj, H, W = obj.shape
+    if tuple(depth.shape) != (B, 1, H, W):
+        raise RuntimeError(f"depth must have shape {(B, 1, H, W)}, got {tuple(depth.shape)}")
+    if obj.dtype != _F32:
+        raise RuntimeError("warp_ego expects a float32 obj")
+    if depth.dtype not in (_F32, _F64):
+        raise RuntimeError(f"depth must be float32 or float64, got {depth.dtype}")
+    dev = obj.device
+    if depth.device != dev:
+        raise RuntimeError("obj and depth must be on one device")
+    P, ik = _ego_camera(B, P, inv_K, dev)
+    with torch.cuda.device(dev):
+        stream = torch.cuda.current_stream(dev)
+        if out is None:
+            output = torch.empty(B, Cobj + 3, H, W, dtype=_F32, device=dev)
+            valid = torch.empty(B, 1, H, W, dtype=_F32, device=dev)
+            collision = torch.empty_like(valid)
+        else:
+            output, valid, collision = out
+        nbytes = _ws_bytes(B, H, W, False)
+        ws = workspace(dev, nbytes, stream) if nbytes else None
+        lib = _native.lib()
+        fn = lib.ofd_fw_warp_ego_f64depth if depth.dtype == _F64 else lib.ofd_fw_warp_ego_f32
+        rc = fn(obj.data_ptr(), Cobj, depth.data_ptr(), P.data_ptr(), ik.data_ptr(), output.data_ptr(),
+                valid.data_ptr(), collision.data_ptr(), B, H, W, ws.data_ptr() if ws is not None else None,
+                ws.numel() if ws is not None else 0, stream.cuda_stream)
+        _native.check(rc, "warp_ego")
     return output, valid, collision

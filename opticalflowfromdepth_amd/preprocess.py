@@ -32,7 +32,7 @@ from torch import nn
 
 from . import synth
 from .fw import FW
-from .ops import inpaint, warp_disparity
+from .ops import ego_flow, inpaint, warp_disparity, warp_ego
 from .synth import fix_warped_depth, get_random, normalize_depth
 
 AUGMENT_SCHEDULE = (0, 5, 6, 7, 1, 5, 6, 7, 2, 5, 6, 7)  # preprocess.py:454
@@ -110,7 +110,15 @@ class Convert:
         T = T1 if T1.dim() == 3 else T1.unsqueeze(0)
         if T.shape[0] != d.shape[0]:
             T = T.expand(d.shape[0], 4, 4)
-        flow = synth.ego_motion_flow(d, T.to(d.device))
+        if d.is_cuda:
+            # the one-kernel flow plane (ops.ego_flow, within 8 ulp of the
+            # reference's arithmetic: tests/test_ego.py)
+            P, ik = synth.projection(d.shape[-2], d.shape[-1], T, d.device)
+            flow = ego_flow(d.contiguous(), P, ik)
+        else:
+            # host tensors (the reference's code accepts them): its own
+            # arithmetic, as restated in synth (pinned by tests/golden)
+            flow = synth.ego_motion_flow(d, T.to(d.device))
         if device is not None:
             flow = flow.to(device)
         return (flow if batched else flow[0]), T1
@@ -371,8 +379,13 @@ class PreprocessPlusAugment(nn.Module):
         img1_depth = fix_warped_depth(img1_depth)
         img1 = inpaint(img1, img1_valid, coll)                                         # :366
 
+        # :372-373 (and :385-387 below): the ego-motion flow plane is kept (it
+        # is a group output); the warp derives the same flow in-kernel and
+        # generates obj's depth / flow channels (bit-identical to
+        # fw(cat(img1, img1_depth, flow12 * -1.0, img1_valid), flow12, img1_depth))
+        P, ik = synth.projection(img0.shape[-2], img0.shape[-1], T1, img0.device)
         flow12, _ = Convert.depth_to_random_flow(img1_depth, T1=T1)                    # :372
-        o, valid, coll = fw(torch.cat((img1, img1_depth, flow12 * -1.0, img1_valid), 1), flow12, img1_depth)
+        o, valid, coll = warp_ego(torch.cat((img1, img1_valid), 1), img1_depth.contiguous(), P, ik)
         img2, img2_depth, back_flow12, fw_img1_valid = o[:, 0:3], o[:, 3:4], o[:, 4:6], o[:, 6:7]
         img2_valid = valid * fw_img1_valid
         img2 = img2 * img2_valid
@@ -382,7 +395,7 @@ class PreprocessPlusAugment(nn.Module):
         img2_depth = fix_warped_depth(img2_depth)
 
         flow03, _ = Convert.depth_to_random_flow(img0_depth, T1=T1)                    # :385
-        o, img3_valid, coll = fw(torch.cat((img0, img0_depth, flow03 * -1.0), 1), flow03, img0_depth)
+        o, img3_valid, coll = warp_ego(img0.to(torch.float32).contiguous(), img0_depth.contiguous(), P, ik)
         img3, img3_depth, back_flow03 = o[:, 0:3], o[:, 3:4], o[:, 4:6]
         img3 = img3 * img3_valid
         img3_depth = img3_depth * img3_valid

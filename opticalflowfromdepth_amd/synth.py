@@ -205,6 +205,15 @@ def disparity_flow(depth: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
     return torch.cat((disparity, torch.zeros_like(disparity)), dim=1) * -1.0
 
 
+def projection(h: int, w: int, T: torch.Tensor, device) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Project3D's P = (K @ T)[:, :3] (geometry.py:57) on ``device`` [B,3,4], and
+    inv_K[:3,:3] (geometry.py:38) as a CPU [3,3] float32 tensor -- the camera
+    inputs of ops.ego_flow / ops.warp_ego."""
+    K, inv_K = intrinsics(h, w)
+    P = torch.matmul(K.to(device).unsqueeze(0), T.to(device))[:, :3, :].contiguous()
+    return P, inv_K[:3, :3].contiguous()
+
+
 def ego_motion_flow(depth: torch.Tensor, T: torch.Tensor) -> torch.Tensor:
     """Convert.depth_to_random_flow (preprocess.py:265-298), batched.
 
