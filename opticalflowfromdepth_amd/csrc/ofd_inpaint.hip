@@ -37,6 +37,8 @@
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
 
 #include "ofd_fw.h"
 #include "ofd_inpaint.h"
@@ -819,6 +821,8 @@ int ofd_inpaint_telea_f32(const float *img, const float *valid, const float *col
             hipLaunchKernelGGL(ip_negate_kernel, dim3(blocks_for(off, 256)), dim3(256), 0, st, w.T, w.list, off);
         for (int L = 1; nring + 2 * (L - 1) < nbins; ++L) {  // holes: patch-interior, then the others
             const unsigned ni = hh[nring + 2 * (L - 1)], nw = hh[nring + 2 * (L - 1) + 1];
+            static const bool dbg = getenv("OFD_IP_DEBUG") != nullptr;  // per-layer sizes (tools/ip_layers.py)
+            if (dbg && ni + nw) fprintf(stderr, "ip layer %d interior %u other %u\n", L, ni, nw);
             const unsigned nbp = blocks_for(ni, 256), nbw = blocks_for(nw, 4);
             if (nbp + nbw)
                 hipLaunchKernelGGL(ip_hole_layer_kernel, dim3(nbp + nbw), dim3(256), 0, st, ch, w.list + off, ni, nbp,

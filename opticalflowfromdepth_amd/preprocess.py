@@ -528,7 +528,8 @@ def main(argv=None) -> None:
     ap.add_argument("--split", default=None, type=int)
     ap.add_argument("--split_id", default=None, type=int)
     ap.add_argument("--epochs", default=2, type=int)
-    ap.add_argument("--batch", default=8, type=int, help="images per batched call")
+    ap.add_argument("--batch", default=64, type=int,
+                    help="images per batched call (larger batches amortise the hole-fill layer latency)")
     ap.add_argument("--out", default="datasets/AugmentedDatasets/synthetic")
     ap.add_argument("--no-augment", action="store_true")
     ap.add_argument("--no-save", action="store_true")

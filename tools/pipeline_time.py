@@ -9,7 +9,7 @@ import torch
 sys.path.insert(0, __file__.rsplit("/tools/", 1)[0])
 from opticalflowfromdepth_amd import preprocess as pp, synth  # noqa: E402
 
-B = int(sys.argv[1]) if len(sys.argv) > 1 else 16
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 H, W = (int(sys.argv[2]), int(sys.argv[3])) if len(sys.argv) > 3 else (768, 1024)
 dev = torch.device("cuda:0")
 seeds = [12345 + i for i in range(B)]
