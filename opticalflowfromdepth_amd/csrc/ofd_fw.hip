@@ -75,7 +75,7 @@ constexpr int SBW = 16, SBH = 4;          // source block = one wave (64 px)
 constexpr int SEGB = 8;                   // source blocks per segment (128 x 4 px)
 constexpr int MAX_TILES_PER_BLOCK = 12;   // wider boxes go through the global path
 constexpr int kSplatU = 2;                // 4-block slots in flight per wave (SPLAT, f32 coords; 3 spills)
-constexpr int kBinSPW = 1;                // segments per BIN wave (2 / 4: 125 / 192 us vs 96 at 64 images)
+constexpr int kBinSPW = 1;                // segments per BIN wave (bin_kernel)
 
 // Default chunk: 64M source pixels (85 images of 768x1024, a ~830 MB slab).
 // Every kernel of a chunk then has a grid many times the resident slots
@@ -560,10 +560,15 @@ __device__ __forceinline__ unsigned quad_min_pk16(unsigned v) {
     return pk_min_u16(v, unsigned(__shfl_xor(int(v), 32)));
 }
 
+// Records: after the quad reduction every lane of quad k holds block k's box,
+// so lanes 4k (k < SEGB) store the 8 block records in ONE 64-byte store
+// instruction, and the segment box is a 3-step xor reduction over the quads
+// (8 readlanes and 9 single-lane stores before: 98 -> 72 us per 64 images,
+// and 76 -> 56 VGPRs, i.e. 8 waves per SIMD).
 template <typename Coords>
 __device__ __forceinline__ void bin_segment(const Coords &co, const float *__restrict__ depth, const ChunkArgs &a,
-                                            int H, int W, int64_t HW, const TileGeom &g, int64_t sgg,
-                                            const typename Coords::V (&x)[2][4], const typename Coords::V (&y)[2][4]) {
+                                               int H, int W, int64_t HW, const TileGeom &g, int64_t sgg,
+                                               const typename Coords::V (&x)[2][4], const typename Coords::V (&y)[2][4]) {
     const Ws &ws = a.ws;
     const int lane = lane_id();
     const int bl = int(sgg / g.nseg);
@@ -572,87 +577,78 @@ __device__ __forceinline__ void bin_segment(const Coords &co, const float *__res
     const int64_t b = a.b0 + bl;
     const int i0 = sgx * (SEGB * SBW) + (lane & 31) * 4;
     const int jh = sby * SBH + (lane >> 5);
-    int tx[2][4], ty[2][4];
+    unsigned mn = 0xFFFFFFFFu, mxi = 0xFFFFFFFFu;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
         const int j = jh + 2 * q;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            tx[q][e] = ty[q][e] = -1;
-            if (i0 + e < W && j < H) co.target(b, i0 + e, j, x[q][e], y[q][e], H, W, tx[q][e], ty[q][e]);
-        }
-    }
-    // per lane: packed (tile x, tile y) min and (0xFFFF - tile x, 0xFFFF - tile y) min
-    unsigned mn = 0xFFFFFFFFu, mxi = 0xFFFFFFFFu;
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-            if (tx[q][e] >= 0) {
-                const unsigned ttx = unsigned(tx[q][e] / TW), tty = unsigned(ty[q][e] / TH);
+            int tx = -1, ty = -1;
+            if (i0 + e < W && j < H) co.target(b, i0 + e, j, x[q][e], y[q][e], H, W, tx, ty);
+            if (tx >= 0) {
+                const unsigned ttx = unsigned(tx / TW), tty = unsigned(ty / TH);
                 mn = pk_min_u16(mn, ttx | (tty << 16));
                 mxi = pk_min_u16(mxi, (0xFFFFu - ttx) | ((0xFFFFu - tty) << 16));
             }
+        }
+    }
     mn = quad_min_pk16(mn);
     mxi = quad_min_pk16(mxi);
-    int s0x = 0x7FFFFFFF, s1x = -1, s0y = 0x7FFFFFFF, s1y = -1;
-    unsigned wide = 0;  // wave-uniform: blocks whose sources go through the key slab
+    const int k = (lane & 31) >> 2;  // this lane's block in the segment
+    const int sbx = sgx * SEGB + k;
+    const bool nonempty = (mn & 0xFFFFu) != 0xFFFFu;
+    const int t0x = int(mn & 0xFFFFu), t0y = int(mn >> 16);
+    const int t1x = int(0xFFFFu - (mxi & 0xFFFFu)), t1y = int(0xFFFFu - (mxi >> 16));
+    const bool is_wide = nonempty && (t1x - t0x + 1) * (t1y - t0y + 1) > MAX_TILES_PER_BLOCK;
+    const bool boxed = nonempty && !is_wide;
+    // segment union of the boxed blocks (quads hold equal values: xor 4, 8, 16)
+    unsigned smn = boxed ? mn : 0xFFFFFFFFu, smx = boxed ? mxi : 0xFFFFFFFFu;
 #pragma unroll
-    for (int k = 0; k < SEGB; ++k) {
-        const int sbx = sgx * SEGB + k;
-        if (sbx >= g.nsbx) break;  // wave-uniform
-        const unsigned bmn = unsigned(__builtin_amdgcn_readlane(int(mn), 4 * k));
-        const unsigned bmx = unsigned(__builtin_amdgcn_readlane(int(mxi), 4 * k));
-        ushort4 rec = empty_box();
-        if ((bmn & 0xFFFFu) != 0xFFFFu) {
-            const int t0x = int(bmn & 0xFFFFu), t0y = int(bmn >> 16);
-            const int t1x = int(0xFFFFu - (bmx & 0xFFFFu)), t1y = int(0xFFFFu - (bmx >> 16));
-            if ((t1x - t0x + 1) * (t1y - t0y + 1) > MAX_TILES_PER_BLOCK) {
-                wide |= 1u << k;  // non-smooth flow: spilled below
-            } else {
-                rec = make_ushort4((unsigned short)t0x, (unsigned short)t1x, (unsigned short)t0y,
-                                   (unsigned short)t1y);
-                s0x = t0x < s0x ? t0x : s0x;
-                s1x = t1x > s1x ? t1x : s1x;
-                s0y = t0y < s0y ? t0y : s0y;
-                s1y = t1y > s1y ? t1y : s1y;
-            }
-        }
-        if (lane == 0) ws.blkrec[int64_t(bl) * g.nsb + int64_t(sby) * g.nsbx + sbx] = rec;
+    for (int m = 4; m < 32; m <<= 1) {
+        smn = pk_min_u16(smn, unsigned(__shfl_xor(int(smn), m)));
+        smx = pk_min_u16(smx, unsigned(__shfl_xor(int(smx), m)));
     }
+    if (lane < 32 && (lane & 3) == 0 && sbx < g.nsbx)
+        ws.blkrec[int64_t(bl) * g.nsb + int64_t(sby) * g.nsbx + sbx] =
+            boxed ? make_ushort4((unsigned short)t0x, (unsigned short)t1x, (unsigned short)t0y, (unsigned short)t1y)
+                  : empty_box();
     if (lane == 0)
-        ws.segrec[sgg] = s1x < 0 ? empty_box()
-                                 : make_ushort4((unsigned short)s0x, (unsigned short)s1x, (unsigned short)s0y,
-                                                (unsigned short)s1y);
-    if (wide == 0u) return;
+        ws.segrec[sgg] = (smn & 0xFFFFu) == 0xFFFFu
+                             ? empty_box()
+                             : make_ushort4((unsigned short)(smn & 0xFFFFu), (unsigned short)(0xFFFFu - (smx & 0xFFFFu)),
+                                            (unsigned short)(smn >> 16), (unsigned short)(0xFFFFu - (smx >> 16)));
+    // wide blocks as a bit mask over k (bit 4k of the ballot of lanes < 32)
+    const unsigned long long wb = __ballot(is_wide && lane < 32 && (lane & 3) == 0);
+    if (wb == 0ull) return;  // wave-uniform
     // non-smooth flow (rare): the wide blocks' sources go to the key slab by
     // global atomic min and flag their target tiles for SPLAT's merge
-#pragma unroll 1
-    for (int k = 0; k < SEGB; ++k) {
-        if (!((wide >> k) & 1u)) continue;
-        const bool mine_lane = ((lane & 31) >> 2) == k;
+    const bool mine_lane = (wb >> (4 * k)) & 1ull;
 #pragma unroll
-        for (int q = 0; q < 2; ++q)
+    for (int q = 0; q < 2; ++q)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const bool ok = mine_lane && tx[q][e] >= 0;
-                const int64_t p = int64_t(jh + 2 * q) * W + i0 + e;
-                const unsigned long long key = ok ? make_key(co.key_depth(b, p, depth), unsigned(p)) : 0ull;
-                wave_run_atomic_min(ws.keys + int64_t(bl) * HW, ok ? ty[q][e] * W + tx[q][e] : -1, key);
-                if (ok) ws.flag[int64_t(bl) * g.ntiles + (ty[q][e] / TH) * g.tilesX + tx[q][e] / TW] = 0u;
-            }
-    }
+        for (int e = 0; e < 4; ++e) {
+            const int j = jh + 2 * q;
+            int tx = -1, ty = -1;
+            if (mine_lane && i0 + e < W && j < H) co.target(b, i0 + e, j, x[q][e], y[q][e], H, W, tx, ty);
+            const bool ok = tx >= 0;
+            const int64_t p = int64_t(j) * W + i0 + e;
+            const unsigned long long key = ok ? make_key(co.key_depth(b, p, depth), unsigned(p)) : 0ull;
+            wave_run_atomic_min(ws.keys + int64_t(bl) * HW, ok ? ty * W + tx : -1, key);
+            if (ok) ws.flag[int64_t(bl) * g.ntiles + (ty / TH) * g.tilesX + tx / TW] = 0u;
+        }
 }
 
 // kSPW segments per wave (consecutive in the image's segment order): every
-// segment's coordinate loads are issued before the first one is folded.
+// segment's coordinate loads are issued before the first one is folded
+// (2 / 4: 0.754 / 0.763 ms per 64-image step vs 0.737 at 1).
 template <typename Coords, bool kVec, int kSPW = 1>
 __global__ __launch_bounds__(kWarpThreads) void bin_kernel(Coords co, const float *__restrict__ depth, ChunkArgs a,
-                                                           int H, int W, int64_t HW, TileGeom g) {
+                                                              int H, int W, int64_t HW, TileGeom g) {
     using V = typename Coords::V;
     const int lane = lane_id();
     const int64_t sg0 = (int64_t(blockIdx.x) * kWaves + (threadIdx.x >> 6)) * kSPW;
     const int64_t nsg = int64_t(a.nimg) * g.nseg;
+    if (sg0 >= nsg) return;  // wave-uniform
     V x[kSPW][2][4], y[kSPW][2][4];
 #pragma unroll
     for (int s = 0; s < kSPW; ++s) {
