@@ -18,7 +18,7 @@ import threading
 import torch  # noqa: F401  -- must precede the CDLL load (shared HIP runtime)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_build", "libofd_fw.so")
+LIB_PATH = os.environ.get("OFD_FW_LIB") or os.path.join(_HERE, "_build", "libofd_fw.so")  # override: probe builds only
 ABI_VERSION = 1
 
 _lock = threading.Lock()
