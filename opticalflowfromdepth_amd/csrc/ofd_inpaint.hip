@@ -348,7 +348,7 @@ constexpr bool need3(int a, int b) {  // in the disk, or a 4-neighbour of a disk
 constexpr int pidx(int a, int b) { return (a + 4) * 9 + (b + 4); }
 
 template <bool kBorder>
-__device__ __forceinline__ void telea_pixel_r3(const Img &m, int y, int x, unsigned L, int64_t p) {
+__device__ __forceinline__ void telea_pixel_r3(const Img &m, int y, int x, unsigned L, int64_t p, int c_lo, int c_hi) {
     const int W = m.W, H = m.H;
     // patch position (a, b) -> in-image flag and (clamped) pixel index; every
     // load below is unconditional, so they all issue before the first use
@@ -394,7 +394,7 @@ __device__ __forceinline__ void telea_pixel_r3(const Img &m, int y, int x, unsig
                             fm_solve(tk[pidx(1, 0)], IN(1, 0), tk[pidx(0, -1)], IN(0, -1)),
                             fm_solve(tk[pidx(-1, 0)], IN(-1, 0), tk[pidx(0, 1)], IN(0, 1)),
                             fm_solve(tk[pidx(1, 0)], IN(1, 0), tk[pidx(0, 1)], IN(0, 1)));
-    m.T[p] = tij;
+    if (c_lo == 0) m.T[p] = tij;
     float gtx, gty;
     if (!IN(0, 1))
         gtx = !IN(0, -1) ? (tk[pidx(0, 1)] - tk[pidx(0, -1)]) * 0.5f : (tk[pidx(0, 1)] - tij);
@@ -422,7 +422,7 @@ __device__ __forceinline__ void telea_pixel_r3(const Img &m, int y, int x, unsig
             wt[pidx(a, b)] = used(a, b) ? w : 0.f;
             s = used(a, b) ? s + w : s;
         }
-    for (int c = 0; c < m.C; ++c) {
+    for (int c = c_lo; c < c_hi; ++c) {
         const float *ob = m.out + int64_t(c) * m.HW;
         const float *ib0 = m.img + int64_t(c) * m.HW;
         float V[81];
@@ -632,21 +632,27 @@ __global__ __launch_bounds__(256) void ip_negate_kernel(float *__restrict__ T, c
 }
 
 // hole layer L: distance, then every channel's Telea colour
+// Patch-interior holes, kCS threads per hole: thread i takes hole i / kCS and
+// the channels c = i % kCS, c + kCS, ... of it.  Every thread of a hole
+// recomputes the same weights (the code / distance patch loads of one hole
+// coalesce into the same lines); only the channel-0 thread writes T.  More,
+// shorter threads: a mid-size layer of ~48 k holes otherwise leaves under one
+// wave per SIMD, each running the whole serial chain of one hole.
+template <int kCS>
 __device__ __forceinline__ void hole_patch(const Chunk &ch, const uint32_t *__restrict__ list, unsigned n, unsigned i,
                                            unsigned L) {
-    if (i >= n) return;
+    const unsigned h = i / unsigned(kCS), c0 = i - h * unsigned(kCS);
+    if (h >= n) return;
     int y, x;
     int64_t p;
-    const Img m = image_of(ch, list[i], y, x, p);
-    telea_pixel_r3<false>(m, y, x, L, p);  // the sort put only radius-3 interior holes here
+    const Img m = image_of(ch, list[h], y, x, p);
+    if (kCS == 1) {
+        telea_pixel_r3<false>(m, y, x, L, p, 0, m.C);  // the sort put only radius-3 interior holes here
+    } else {
+        for (int c = int(c0); c < m.C; c += kCS) telea_pixel_r3<false>(m, y, x, L, p, c, c + 1);  // C >= 1
+    }
 }
 
-// The other holes (image border, or a radius other than 3): one wave per
-// hole.  Lane j evaluates position j of the (2r+1)^2 window raster (64 at a
-// time) -- flags, distance, weight and its channel terms, all loads
-// independent -- and the wave folds the terms in raster order with readlane,
-// so every sum is the sequential one (icvTeleaInpaintFMM's (k, l) loop), bit
-// for bit.
 __device__ __forceinline__ float rl(float v, int j) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
 }
@@ -738,14 +744,158 @@ __device__ __forceinline__ void hole_wave(const Chunk &ch, const uint32_t *__res
     if (lane == 0) m.T[p] = tij;
 }
 
+// Wave per hole, radius <= 3: the same arithmetic as hole_wave, but the 9x9
+// patch around the hole (INSIDE flags, distances, and per channel group the
+// sample() values) is loaded into LDS in ONE round of unconditional, clamped
+// loads (entry e = lane, lane + 64).  hole_wave's chain of dependent rounds
+// (list -> code -> T -> code -> sample code -> value) becomes list -> patch.
+constexpr int kPatch = 9, kPatchN = kPatch * kPatch;
+struct WavePatch {
+    int fl[kPatchN];                // bit 0: inside the image, bit 1: INSIDE (hole of layer >= L)
+    float t[kPatchN];               // T (raw)
+    int sv[kChanGroup][kPatchN];    // sample() of the current channel group
+};
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ void hole_wave_lds(const Chunk &ch, const uint32_t *__restrict__ list, unsigned n,
+                                              unsigned i, unsigned L, int range, WavePatch &P) {
+    if (i >= n) return;  // wave-uniform
+    const int lane = threadIdx.x & 63;
+    int y, x;
+    int64_t p;
+    const Img m = image_of(ch, list[i], y, x, p);
+    const int H = m.H, W = m.W, R = range, D = 2 * range + 1, npos = D * D;
+    int64_t qe[2];
+    unsigned hge[2];  // sample()'s test: hole of layer >= L
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int e = lane + 64 * u;
+        const int k = y - 4 + e / kPatch, l = x - 4 + e % kPatch;
+        const bool inimg = k >= 0 && k < H && l >= 0 && l < W;
+        const int kc = min(max(k, 0), H - 1), lc = min(max(l, 0), W - 1);
+        qe[u] = int64_t(kc) * W + lc;
+        if (e < kPatchN) {
+            const unsigned cd = m.code[qe[u]];
+            const float tq = m.T[qe[u]];
+            hge[u] = ((cd & C_HOLE) && (cd & LAY) >= L) ? 1u : 0u;
+            P.fl[e] = (inimg ? 1 : 0) | ((inimg && hge[u]) ? 2 : 0);
+            P.t[e] = tq;
+        }
+    }
+    wave_lds_sync();
+    auto IN = [&](int e) -> bool { return (P.fl[e] & 2) != 0; };
+    auto TV = [&](int e, bool &in) -> float {
+        const int f = P.fl[e];
+        in = (f & 2) != 0;
+        return (in || !(f & 1)) ? T_FAR : P.t[e];
+    };
+    constexpr int ctr = 4 * kPatch + 4;
+    bool iu, id, il, ir;
+    const float tu = TV(ctr - kPatch, iu), td = TV(ctr + kPatch, id);
+    const float tl = TV(ctr - 1, il), tr = TV(ctr + 1, ir);
+    const float tij = min4f(fm_solve(tu, iu, tl, il), fm_solve(td, id, tl, il), fm_solve(tu, iu, tr, ir),
+                            fm_solve(td, id, tr, ir));
+    float gtx, gty;
+    if (!ir)
+        gtx = !il ? (tr - tl) * 0.5f : (tr - tij);
+    else
+        gtx = !il ? (tij - tl) : 0.f;
+    if (!id)
+        gty = !iu ? (td - tu) * 0.5f : (td - tij);
+    else
+        gty = !iu ? (tij - tu) : 0.f;
+    for (int c0 = 0; c0 < m.C; c0 += kChanGroup) {
+        const int nc = min(kChanGroup, m.C - c0);
+        if (c0 > 0) wave_lds_sync();  // the previous group's reads are done
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int e = lane + 64 * u;
+            if (e < kPatchN)
+                for (int c = 0; c < nc; ++c) {
+                    const int cc = c0 + c;
+                    const float vo = m.out[int64_t(cc) * m.HW + qe[u]], vi = m.img[int64_t(cc) * m.HW + qe[u]];
+                    P.sv[c][e] = hge[u] ? int(to_u8(vi)) : int(vo);
+                }
+        }
+        wave_lds_sync();
+        float Ia[kChanGroup], Jx[kChanGroup], Jy[kChanGroup];
+#pragma unroll
+        for (int c = 0; c < kChanGroup; ++c) Ia[c] = Jx[c] = Jy[c] = 0.f;
+        float s = 1.0e-20f;
+        // npos <= 49: one pass
+        const int idx = lane;
+        const int k = y - R + idx / D, l = x - R + idx % D;
+        const int pk = 4 - R + idx / D, pl = 4 - R + idx % D, e = pk * kPatch + pl;
+        bool valid = idx < npos && k >= 0 && k < H && l >= 0 && l < W && (l - x) * (l - x) + (k - y) * (k - y) <= R * R;
+        valid = valid && !IN(e);
+        float w = 0.f, ti[kChanGroup], tx[kChanGroup], ty[kChanGroup];
+#pragma unroll
+        for (int c = 0; c < kChanGroup; ++c) ti[c] = tx[c] = ty[c] = 0.f;
+        if (valid) {
+            const int km = pk + (k == 0), kp = pk - (k == H - 1), lm = pl + (l == 0), lp = pl - (l == W - 1);
+            const float ry = float(y - k), rx = float(x - l);
+            const float len2 = rx * rx + ry * ry;
+            const float dst = float(1. / (double(len2) * sqrt(double(len2))));
+            const float lev = float(1. / (1 + fabs(double(P.t[e] - tij))));
+            float dir = rx * gtx + ry * gty;
+            if (fabs(double(dir)) <= 0.01) dir = 0.000001f;
+            w = float(fabs(double(dst * lev * dir)));
+            const bool nr = !IN(e + 1), nl = !IN(e - 1), nd = !IN(e + kPatch), nu = !IN(e - kPatch);
+            auto S = [&](int c, int a, int b) -> int { return P.sv[c][a * kPatch + b]; };
+            for (int c = 0; c < nc; ++c) {
+                float gix, giy;
+                if (nr)
+                    gix = nl ? float(S(c, km, lp + 1) - S(c, km, lm - 1)) * 2.0f : float(S(c, km, lp + 1) - S(c, km, lm));
+                else
+                    gix = nl ? float(S(c, km, lp) - S(c, km, lm - 1)) : 0.f;
+                if (nd)
+                    giy = nu ? float(S(c, kp + 1, lm) - S(c, km - 1, lm)) * 2.0f : float(S(c, kp + 1, lm) - S(c, km, lm));
+                else
+                    giy = nu ? float(S(c, kp, lm) - S(c, km - 1, lm)) : 0.f;
+                ti[c] = w * float(S(c, km, lm));
+                tx[c] = w * (gix * rx);
+                ty[c] = w * (giy * ry);
+            }
+        }
+        const uint64_t vm = __ballot(valid);
+        for (int j = 0; j < 64; ++j) {
+            if (!((vm >> j) & 1ull)) continue;  // uniform
+            for (int c = 0; c < nc; ++c) {
+                Ia[c] += rl(ti[c], j);
+                Jx[c] -= rl(tx[c], j);
+                Jy[c] -= rl(ty[c], j);
+            }
+            s += rl(w, j);
+        }
+        if (lane == 0) {
+            for (int c = 0; c < nc; ++c) {
+                const float sat = float(double(Ia[c] / s) +
+                                        double(Jx[c] + Jy[c]) / (sqrt(double(Jx[c] * Jx[c] + Jy[c] * Jy[c])) + double(1.0e-20f)) +
+                                        double(0.5f));
+                m.out[(c0 + c) * m.HW + p] = float(sat_u8(sat));
+            }
+        }
+    }
+    if (lane == 0) m.T[p] = tij;
+}
+
 // One launch per hole layer: blocks [0, nbp) take the patch-interior holes
 // (thread per hole), the rest the others (wave per hole).  The two sets of a
 // layer are independent, so they share the launch; every block runs one path.
+template <int kCS, bool kWaveLds = true>
 __global__ __launch_bounds__(256) void ip_hole_layer_kernel(Chunk ch, const uint32_t *__restrict__ lp, unsigned np,
                                                             unsigned nbp, const uint32_t *__restrict__ lw, unsigned nw,
                                                             unsigned L, int range) {
+    __shared__ WavePatch patch[4];
     if (blockIdx.x < nbp)
-        hole_patch(ch, lp, np, blockIdx.x * 256u + threadIdx.x, L);
+        hole_patch<kCS>(ch, lp, np, blockIdx.x * 256u + threadIdx.x, L);
+    else if (range <= 3 && kWaveLds)
+        hole_wave_lds(ch, lw, nw, (blockIdx.x - nbp) * 4u + (threadIdx.x >> 6), L, range, patch[threadIdx.x >> 6]);
     else
         hole_wave(ch, lw, nw, (blockIdx.x - nbp) * 4u + (threadIdx.x >> 6), L, range);
 }
@@ -823,10 +973,26 @@ int ofd_inpaint_telea_f32(const float *img, const float *valid, const float *col
             const unsigned ni = hh[nring + 2 * (L - 1)], nw = hh[nring + 2 * (L - 1) + 1];
             static const bool dbg = getenv("OFD_IP_DEBUG") != nullptr;  // per-layer sizes (tools/ip_layers.py)
             if (dbg && ni + nw) fprintf(stderr, "ip layer %d interior %u other %u\n", L, ni, nw);
-            const unsigned nbp = blocks_for(ni, 256), nbw = blocks_for(nw, 4);
-            if (nbp + nbw)
-                hipLaunchKernelGGL(ip_hole_layer_kernel, dim3(nbp + nbw), dim3(256), 0, st, ch, w.list + off, ni, nbp,
-                                   w.list + off + ni, nw, unsigned(L), r);
+            static const int cs = [] {  // probe knob OFD_IP_CS: threads per interior hole (1 or 3)
+                const char *e = getenv("OFD_IP_CS");
+                return e && atoi(e) == 1 ? 1 : 3;
+            }();
+            static const bool wlds = [] {  // probe knob OFD_IP_WLDS=0: border holes on the global-load wave path
+                const char *e = getenv("OFD_IP_WLDS");
+                return !(e && atoi(e) == 0);
+            }();
+            const unsigned nbp = blocks_for(ni * unsigned(cs), 256), nbw = blocks_for(nw, 4);
+            if (nbp + nbw) {
+                if (cs == 3 && !wlds)
+                    hipLaunchKernelGGL((ip_hole_layer_kernel<3, false>), dim3(nbp + nbw), dim3(256), 0, st, ch,
+                                       w.list + off, ni, nbp, w.list + off + ni, nw, unsigned(L), r);
+                else if (cs == 3)
+                    hipLaunchKernelGGL(ip_hole_layer_kernel<3>, dim3(nbp + nbw), dim3(256), 0, st, ch, w.list + off, ni,
+                                       nbp, w.list + off + ni, nw, unsigned(L), r);
+                else
+                    hipLaunchKernelGGL(ip_hole_layer_kernel<1>, dim3(nbp + nbw), dim3(256), 0, st, ch, w.list + off, ni,
+                                       nbp, w.list + off + ni, nw, unsigned(L), r);
+            }
             off += ni + nw;
         }
     }
