@@ -56,7 +56,8 @@ constexpr int DINF = 0x3FFF;  // distance "infinity" in the transforms (> H + W)
 constexpr int kMaxHW = 4096;  // H + W limit: layers fit 13 bits, 2 bins per layer fit LDS
 constexpr int kMaxRange = 100;
 constexpr int kMaxBins = 2 * kMaxHW + 2 * kMaxRange;
-constexpr int kChanGroup = 4;  // channels accumulated together per window pass
+constexpr int kChanGroup = 4;
+constexpr unsigned kCsSplitMax = 262144;  // interior holes of a layer above which one thread takes a whole hole  // channels accumulated together per window pass
 
 inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
@@ -128,27 +129,62 @@ __global__ __launch_bounds__(256) void ip_prep_kernel(const float *__restrict__ 
 
 // ---------------------------------------------------------------- COLS
 // gcol = (vertical distance to the nearest known pixel) | (to the nearest hole) << 16
-__global__ __launch_bounds__(256) void ip_cols_kernel(const uint16_t *__restrict__ code, uint32_t *__restrict__ gcol,
-                                                      int H, int W) {
-    const int x = blockIdx.x * 256 + threadIdx.x;
-    if (x >= W) return;
+// Workgroup = 64 columns x kColSegs row segments; thread (segment, column).
+// Pass 1 sweeps the segment downwards with segment-local state (DINF where
+// the segment has no known pixel / hole above), and records the segment's
+// first and last known / hole rows in LDS; pass 2 sweeps upwards with the
+// state entering from the segments below, patches the DINF entries with the
+// state entering from above, and takes the min of both directions.  Same
+// values as one sequential sweep per column (thread per column before:
+// 620 us per 64 images at one wave per SIMD).
+constexpr int kColSegs = 8;
+__global__ __launch_bounds__(64 * kColSegs) void ip_cols_kernel(const uint16_t *__restrict__ code,
+                                                                 uint32_t *__restrict__ gcol, int H, int W) {
+    __shared__ int lastk[kColSegs][64], lasth[kColSegs][64], firstk[kColSegs][64], firsth[kColSegs][64];
+    const int cx = threadIdx.x & 63, sg = threadIdx.x >> 6;
+    const int x = blockIdx.x * 64 + cx;
+    const int SL = (H + kColSegs - 1) / kColSegs, y0 = min(sg * SL, H), y1 = min(y0 + SL, H);
     const int64_t HW = int64_t(H) * W, bl = blockIdx.y;
     const uint16_t *cb = code + bl * HW;
     uint32_t *gb = gcol + bl * HW;
-    int lk = -DINF, lh = -DINF;
-    for (int y = 0; y < H; ++y) {
-        const bool hole = cb[int64_t(y) * W + x] & C_HOLE;
-        if (hole) lh = y; else lk = y;
-        const int gk = min(y - lk, DINF), gh = min(y - lh, DINF);
-        gb[int64_t(y) * W + x] = uint32_t(gk) | (uint32_t(gh) << 16);
+    int lk = -DINF, lh = -DINF, fk = 2 * DINF, fh = 2 * DINF;
+    if (x < W)
+        for (int y = y0; y < y1; ++y) {
+            const bool hole = cb[int64_t(y) * W + x] & C_HOLE;
+            if (hole) {
+                lh = y;
+                fh = min(fh, y);
+            } else {
+                lk = y;
+                fk = min(fk, y);
+            }
+            const int gk = min(y - lk, DINF), gh = min(y - lh, DINF);
+            gb[int64_t(y) * W + x] = uint32_t(gk) | (uint32_t(gh) << 16);
+        }
+    lastk[sg][cx] = lk;
+    lasth[sg][cx] = lh;
+    firstk[sg][cx] = fk;
+    firsth[sg][cx] = fh;
+    __syncthreads();
+    int lk_in = -DINF, lh_in = -DINF, nk = 2 * DINF, nh = 2 * DINF;
+    for (int t = 0; t < sg; ++t) {
+        lk_in = max(lk_in, lastk[t][cx]);
+        lh_in = max(lh_in, lasth[t][cx]);
     }
-    int nk = 2 * DINF, nh = 2 * DINF;
-    for (int y = H - 1; y >= 0; --y) {
+    for (int t = kColSegs - 1; t > sg; --t) {
+        nk = min(nk, firstk[t][cx]);
+        nh = min(nh, firsth[t][cx]);
+    }
+    if (x >= W) return;
+    for (int y = y1 - 1; y >= y0; --y) {
         const int64_t p = int64_t(y) * W + x;
         const bool hole = cb[p] & C_HOLE;
         if (hole) nh = y; else nk = y;
         const uint32_t g = gb[p];
-        const int gk = min(int(g & 0xFFFFu), min(nk - y, DINF)), gh = min(int(g >> 16), min(nh - y, DINF));
+        int fwk = int(g & 0xFFFFu), fwh = int(g >> 16);
+        if (fwk == DINF) fwk = min(y - lk_in, DINF);
+        if (fwh == DINF) fwh = min(y - lh_in, DINF);
+        const int gk = min(fwk, min(nk - y, DINF)), gh = min(fwh, min(nh - y, DINF));
         gb[p] = uint32_t(gk) | (uint32_t(gh) << 16);
     }
 }
@@ -887,14 +923,14 @@ __device__ __forceinline__ void hole_wave_lds(const Chunk &ch, const uint32_t *_
 // One launch per hole layer: blocks [0, nbp) take the patch-interior holes
 // (thread per hole), the rest the others (wave per hole).  The two sets of a
 // layer are independent, so they share the launch; every block runs one path.
-template <int kCS, bool kWaveLds = true>
+template <int kCS>
 __global__ __launch_bounds__(256) void ip_hole_layer_kernel(Chunk ch, const uint32_t *__restrict__ lp, unsigned np,
                                                             unsigned nbp, const uint32_t *__restrict__ lw, unsigned nw,
                                                             unsigned L, int range) {
     __shared__ WavePatch patch[4];
     if (blockIdx.x < nbp)
         hole_patch<kCS>(ch, lp, np, blockIdx.x * 256u + threadIdx.x, L);
-    else if (range <= 3 && kWaveLds)
+    else if (range <= 3)
         hole_wave_lds(ch, lw, nw, (blockIdx.x - nbp) * 4u + (threadIdx.x >> 6), L, range, patch[threadIdx.x >> 6]);
     else
         hole_wave(ch, lw, nw, (blockIdx.x - nbp) * 4u + (threadIdx.x >> 6), L, range);
@@ -941,7 +977,7 @@ int ofd_inpaint_telea_f32(const float *img, const float *valid, const float *col
         const int64_t total = nb * HW;
         hipLaunchKernelGGL(ip_prep_kernel, dim3(unsigned((W + 63) / 64), unsigned((H + 3) / 4), unsigned(nb)),
                            dim3(256), 0, st, img, valid, collision, out, w.code, int(C), int(H), int(W), b0);
-        hipLaunchKernelGGL(ip_cols_kernel, dim3(unsigned((W + 255) / 256), unsigned(nb)), dim3(256), 0, st, w.code,
+        hipLaunchKernelGGL(ip_cols_kernel, dim3(unsigned((W + 63) / 64), unsigned(nb)), dim3(64 * kColSegs), 0, st, w.code,
                            w.gcol, int(H), int(W));
         hipLaunchKernelGGL(ip_rows_kernel, dim3(unsigned((H + 3) / 4), unsigned(nb)), dim3(256), 0, st, w.code, w.T,
                            w.gcol, w.list, int(H), int(W), r);
@@ -977,20 +1013,16 @@ int ofd_inpaint_telea_f32(const float *img, const float *valid, const float *col
                 const char *e = getenv("OFD_IP_CS");
                 return e && atoi(e) == 1 ? 1 : 3;
             }();
-            static const bool wlds = [] {  // probe knob OFD_IP_WLDS=0: border holes on the global-load wave path
-                const char *e = getenv("OFD_IP_WLDS");
-                return !(e && atoi(e) == 0);
-            }();
-            const unsigned nbp = blocks_for(ni * unsigned(cs), 256), nbw = blocks_for(nw, 4);
+            // a big layer is throughput-bound: one thread per hole (the channel split
+            // recomputes the weights per channel); small layers are latency-bound
+            const int csl = ni > kCsSplitMax ? 1 : cs;
+            const unsigned nbp = blocks_for(ni * unsigned(csl), 256), nbw = blocks_for(nw, 4);
             if (nbp + nbw) {
-                if (cs == 3 && !wlds)
-                    hipLaunchKernelGGL((ip_hole_layer_kernel<3, false>), dim3(nbp + nbw), dim3(256), 0, st, ch,
-                                       w.list + off, ni, nbp, w.list + off + ni, nw, unsigned(L), r);
-                else if (cs == 3)
-                    hipLaunchKernelGGL(ip_hole_layer_kernel<3>, dim3(nbp + nbw), dim3(256), 0, st, ch, w.list + off, ni,
+                if (csl == 1)
+                    hipLaunchKernelGGL(ip_hole_layer_kernel<1>, dim3(nbp + nbw), dim3(256), 0, st, ch, w.list + off, ni,
                                        nbp, w.list + off + ni, nw, unsigned(L), r);
                 else
-                    hipLaunchKernelGGL(ip_hole_layer_kernel<1>, dim3(nbp + nbw), dim3(256), 0, st, ch, w.list + off, ni,
+                    hipLaunchKernelGGL(ip_hole_layer_kernel<3>, dim3(nbp + nbw), dim3(256), 0, st, ch, w.list + off, ni,
                                        nbp, w.list + off + ni, nw, unsigned(L), r);
             }
             off += ni + nw;
