@@ -127,6 +127,54 @@ __global__ __launch_bounds__(256) void ip_prep_kernel(const float *__restrict__ 
     for (int c = 0; c < C; ++c) ob[c * HW + p] = float(to_u8(ib[c * HW + p]));
 }
 
+// Four consecutive pixels per thread (W % 4 == 0, 16-byte aligned planes):
+// the 3x3 neighbourhood of the quad is 3 rows x 6 columns of valid /
+// collision, loaded as one float4 plus two edge values per row (18 loads per
+// 4 pixels instead of 18 per pixel), and the C channel planes move as float4.
+__global__ __launch_bounds__(256) void ip_prep4_kernel(const float *__restrict__ img, const float *__restrict__ valid,
+                                                       const float *__restrict__ coll, float *__restrict__ out,
+                                                       uint16_t *__restrict__ code, int C, int H, int W, int64_t b0) {
+    const int x = (blockIdx.x * 64 + (threadIdx.x & 63)) * 4, y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (x >= W || y >= H) return;
+    const int64_t HW = int64_t(H) * W, bl = blockIdx.z, b = b0 + bl;
+    const float *v = valid + b * HW, *cl = coll + b * HW;
+    const int64_t p = int64_t(y) * W + x;
+    unsigned mrow[3] = {0u, 0u, 0u};  // bit k: M at column x - 1 + k (0 outside the image)
+    float vc[4];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        const int yy = y - 1 + r;
+        if (yy < 0 || yy >= H) continue;
+        const int64_t q = int64_t(yy) * W + x;
+        const float4 a = *reinterpret_cast<const float4 *>(v + q), c = *reinterpret_cast<const float4 *>(cl + q);
+        unsigned m = ((a.x != c.x) ? 2u : 0u) | ((a.y != c.y) ? 4u : 0u) | ((a.z != c.z) ? 8u : 0u) |
+                     ((a.w != c.w) ? 16u : 0u);
+        if (x > 0) m |= (v[q - 1] != cl[q - 1]) ? 1u : 0u;
+        if (x + 4 < W) m |= (v[q + 4] != cl[q + 4]) ? 32u : 0u;
+        mrow[r] = m;
+        if (r == 1) { vc[0] = a.x; vc[1] = a.y; vc[2] = a.z; vc[3] = a.w; }
+    }
+    const unsigned mo = mrow[0] | mrow[1] | mrow[2];
+    ushort4 cd;
+    unsigned short *cde = reinterpret_cast<unsigned short *>(&cd);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const unsigned mp = (mo >> e) & 7u ? 1u : 0u;
+        const unsigned M = (mrow[1] >> (e + 1)) & 1u;
+        const unsigned P = mp == M ? 1u : 0u;
+        const unsigned hp = to_u8(vc[e] * float(P));
+        cde[e] = hp != 1u ? uint16_t(C_HOLE) : uint16_t(0);
+    }
+    *reinterpret_cast<ushort4 *>(code + bl * HW + p) = cd;
+    const float *ib = img + b * int64_t(C) * HW;
+    float *ob = out + b * int64_t(C) * HW;
+    for (int c = 0; c < C; ++c) {
+        const float4 a = *reinterpret_cast<const float4 *>(ib + c * HW + p);
+        *reinterpret_cast<float4 *>(ob + c * HW + p) =
+            make_float4(float(to_u8(a.x)), float(to_u8(a.y)), float(to_u8(a.z)), float(to_u8(a.w)));
+    }
+}
+
 // ---------------------------------------------------------------- COLS
 // gcol = (vertical distance to the nearest known pixel) | (to the nearest hole) << 16
 // Workgroup = 64 columns x kColSegs row segments; thread (segment, column).
@@ -975,8 +1023,15 @@ int ofd_inpaint_telea_f32(const float *img, const float *valid, const float *col
     for (int64_t b0 = 0; b0 < B; b0 += G) {
         const int64_t nb = B - b0 < G ? B - b0 : G;
         const int64_t total = nb * HW;
-        hipLaunchKernelGGL(ip_prep_kernel, dim3(unsigned((W + 63) / 64), unsigned((H + 3) / 4), unsigned(nb)),
-                           dim3(256), 0, st, img, valid, collision, out, w.code, int(C), int(H), int(W), b0);
+        const bool vec4 = W % 4 == 0 && ((reinterpret_cast<uintptr_t>(img) | reinterpret_cast<uintptr_t>(valid) |
+                                          reinterpret_cast<uintptr_t>(collision) | reinterpret_cast<uintptr_t>(out)) &
+                                         15u) == 0;
+        if (vec4)
+            hipLaunchKernelGGL(ip_prep4_kernel, dim3(unsigned((W / 4 + 63) / 64), unsigned((H + 3) / 4), unsigned(nb)),
+                               dim3(256), 0, st, img, valid, collision, out, w.code, int(C), int(H), int(W), b0);
+        else
+            hipLaunchKernelGGL(ip_prep_kernel, dim3(unsigned((W + 63) / 64), unsigned((H + 3) / 4), unsigned(nb)),
+                               dim3(256), 0, st, img, valid, collision, out, w.code, int(C), int(H), int(W), b0);
         hipLaunchKernelGGL(ip_cols_kernel, dim3(unsigned((W + 63) / 64), unsigned(nb)), dim3(64 * kColSegs), 0, st, w.code,
                            w.gcol, int(H), int(W));
         hipLaunchKernelGGL(ip_rows_kernel, dim3(unsigned((H + 3) / 4), unsigned(nb)), dim3(256), 0, st, w.code, w.T,
