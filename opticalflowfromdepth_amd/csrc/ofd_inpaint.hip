@@ -344,6 +344,87 @@ __global__ __launch_bounds__(256) void ip_rows_kernel(uint16_t *__restrict__ cod
     }
 }
 
+// ROWS for W <= 64 * kRowRegs: the whole row lives in registers (kRowRegs
+// values per lane), so every gcol / code load of the row issues up front and
+// the forward results never round-trip through tmp.  Same arithmetic as
+// ip_rows_kernel (which ran one dependent load per 64-column step).
+constexpr int kRowRegs = 16;
+__global__ __launch_bounds__(256) void ip_rows_reg_kernel(uint16_t *__restrict__ code, float *__restrict__ T,
+                                                          const uint32_t *__restrict__ gcol, int H, int W, int r) {
+    const int y = blockIdx.x * 4 + int(threadIdx.x >> 6);
+    if (y >= H) return;  // wave-uniform
+    const int lane = threadIdx.x & 63;
+    const int64_t HW = int64_t(H) * W, bl = blockIdx.y;
+    const int64_t row = bl * HW + int64_t(y) * W;
+    const int nst = (W + 63) / 64;
+    uint32_t g[kRowRegs], f[kRowRegs];
+    bool hole[kRowRegs];
+#pragma unroll
+    for (int s = 0; s < kRowRegs; ++s) {
+        const int x = s * 64 + lane;
+        g[s] = 0u;
+        hole[s] = false;
+        if (s < nst && x < W) {
+            g[s] = gcol[row + x];
+            hole[s] = code[row + x] & C_HOLE;
+        }
+    }
+    int ck = kBig, ch = kBig, cl = -kBig;
+#pragma unroll
+    for (int s = 0; s < kRowRegs; ++s) {
+        const int x = s * 64 + lane;
+        int vk = kBig, vh = kBig, lo = -kBig;
+        if (s < nst && x < W) {  // steps past the row hold the scan identities
+            const int gk = int(g[s] & 0xFFFFu), gh = int(g[s] >> 16);
+            vk = gk - x;
+            vh = gh - x;
+            lo = gh <= r ? x : -kBig;
+        }
+        vk = min(wave_prefix_min(vk), ck);
+        vh = min(wave_prefix_min(vh), ch);
+        lo = max(wave_prefix_max(lo), cl);
+        ck = __shfl(vk, 63);
+        ch = __shfl(vh, 63);
+        cl = __shfl(lo, 63);
+        f[s] = uint32_t(x + vk) | (uint32_t(x + vh) << 16) | (x - lo <= r ? 0x80000000u : 0u);
+    }
+    int sk = kBig, sh = kBig, sn = kBig;
+#pragma unroll
+    for (int s = kRowRegs - 1; s >= 0; --s) {
+        const int x = s * 64 + lane;
+        int uk = kBig, uh = kBig, nx = kBig;
+        if (s < nst && x < W) {
+            uk = int(f[s] & 0x7FFFu) + x;
+            uh = int((f[s] >> 16) & 0x7FFFu) + x;
+            nx = int(g[s] >> 16) <= r ? x : kBig;
+        }
+        uk = min(wave_suffix_min(uk), sk);
+        uh = min(wave_suffix_min(uh), sh);
+        nx = min(wave_suffix_min(nx), sn);
+        sk = __shfl(uk, 0);
+        sh = __shfl(uh, 0);
+        sn = __shfl(nx, 0);
+        if (s < nst && x < W) {
+            const int bk = uk - x, bh = uh - x;
+            const bool near = (f[s] >> 31) || nx - x <= r;
+            unsigned cd;
+            float t = T_FAR;
+            if (hole[s]) {
+                cd = C_HOLE | unsigned(bk >= int(LAY_INF) ? LAY_INF : bk);
+            } else if (bh == 1) {
+                cd = 0u;  // band
+                t = 0.f;
+            } else if (near && bh < DINF) {
+                cd = C_RING | unsigned(bh - 1);
+            } else {
+                cd = C_FAR;
+            }
+            code[row + x] = uint16_t(cd);
+            T[row + x] = t;
+        }
+    }
+}
+
 // ---------------------------------------------------------------- TELEA
 struct Img {  // one image's state inside the TELEA workgroup
     const uint16_t *code;
@@ -1034,7 +1115,11 @@ int ofd_inpaint_telea_f32(const float *img, const float *valid, const float *col
                                dim3(256), 0, st, img, valid, collision, out, w.code, int(C), int(H), int(W), b0);
         hipLaunchKernelGGL(ip_cols_kernel, dim3(unsigned((W + 63) / 64), unsigned(nb)), dim3(64 * kColSegs), 0, st, w.code,
                            w.gcol, int(H), int(W));
-        hipLaunchKernelGGL(ip_rows_kernel, dim3(unsigned((H + 3) / 4), unsigned(nb)), dim3(256), 0, st, w.code, w.T,
+        if (W <= 64 * kRowRegs)
+            hipLaunchKernelGGL(ip_rows_reg_kernel, dim3(unsigned((H + 3) / 4), unsigned(nb)), dim3(256), 0, st, w.code,
+                               w.T, w.gcol, int(H), int(W), r);
+        else
+            hipLaunchKernelGGL(ip_rows_kernel, dim3(unsigned((H + 3) / 4), unsigned(nb)), dim3(256), 0, st, w.code, w.T,
                            w.gcol, w.list, int(H), int(W), r);
         hipError_t e = hipMemsetAsync(hist, 0, size_t(kMaxBins) * 4, st);
         if (e != hipSuccess) return int(e);

@@ -16,6 +16,7 @@ hl = [dur(r) for r in last if "hole_layer" in r["Kernel_Name"]]
 print(f"last call: span {span:.0f} us, {len(last)} launches, hole layers {len(hl)}: sum {sum(hl):.0f} us, "
       f"first {[round(x) for x in hl[:6]]}, median {sorted(hl)[len(hl) // 2]:.1f} us")
 for name in ("prep", "cols", "rows", "hist", "scan", "scatter", "ring_layer", "negate"):
-    t = [dur(r) for r in last if f"ip_{name}_kernel" in r["Kernel_Name"] or f"ip_{name}4_kernel" in r["Kernel_Name"]]
+    t = [dur(r) for r in last if f"ip_{name}_kernel" in r["Kernel_Name"] or f"ip_{name}4_kernel" in r["Kernel_Name"]
+         or f"ip_{name}_reg_kernel" in r["Kernel_Name"]]
     if t:
         print(f"  {name:10s} {sum(t):8.1f} us ({len(t)} launches)")
