@@ -665,8 +665,9 @@ constexpr int kSortSpan = 16384;  // pixels per sort workgroup
 // register-patch kernel takes (radius 3, window and halo inside the image),
 // nring + 2(l-1) + 1 for the others (one wave per hole)
 __device__ __forceinline__ bool patch_interior(int64_t e, int64_t HW, int H, int W, bool r3) {
-    const int64_t p = e % HW;
-    const int y = int(p / W), x = int(p - int64_t(y) * W);
+    // entries fit 31 bits (gcap in ofd_inpaint_telea_f32): 32-bit division
+    const unsigned p = unsigned(e) % unsigned(HW);
+    const int y = int(p / unsigned(W)), x = int(p - unsigned(y) * unsigned(W));
     return r3 && y >= 4 && y < H - 4 && x >= 4 && x < W - 4;
 }
 __device__ __forceinline__ int bin_of(unsigned cd, int nring, int64_t e, int64_t HW, int H, int W, bool r3) {
@@ -762,10 +763,12 @@ struct Chunk {
 };
 
 __device__ __forceinline__ Img image_of(const Chunk &ch, uint32_t e, int &y, int &x, int64_t &p) {
-    const int64_t bl = int64_t(e) / ch.HW, b = ch.b0 + bl;
-    p = int64_t(e) - bl * ch.HW;
-    y = int(p / ch.W);
-    x = int(p - int64_t(y) * ch.W);
+    // entries fit 31 bits (gcap in ofd_inpaint_telea_f32): 32-bit divisions
+    const unsigned ble = e / unsigned(ch.HW), pe = e - ble * unsigned(ch.HW);
+    const int64_t bl = int64_t(ble), b = ch.b0 + bl;
+    p = int64_t(pe);
+    y = int(pe / unsigned(ch.W));
+    x = int(pe - unsigned(y) * unsigned(ch.W));
     Img m;
     m.code = ch.code + bl * ch.HW;
     m.T = ch.T + bl * ch.HW;
