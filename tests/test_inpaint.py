@@ -124,6 +124,12 @@ def _gpu_cases():
         img = rng.integers(0, 256, (1, 3, h, w)).astype(np.float32)
         v = (rng.random((1, 1, h, w)) < 0.5).astype(np.float32)
         cases.append((f"tiny{h}x{w}", img, v, np.zeros_like(v), 3))
+    # wide rows: W > 1024 takes the chunked ROWS kernel (W % 4 == 0: PREP4;
+    # W % 4 != 0: the per-pixel PREP), both beside the register ROWS path
+    for h, w in ((12, 1100), (10, 1030)):
+        img = rng.integers(0, 256, (2, 3, h, w)).astype(np.float32)
+        v = (rng.random((2, 1, h, w)) < 0.7).astype(np.float32)
+        cases.append((f"wide{h}x{w}", img, v, np.zeros_like(v), 3))
     h, w = 40, 50
     img = smooth_image(h, w, 9)[None]
     v = np.ones((1, 1, h, w), np.float32)
