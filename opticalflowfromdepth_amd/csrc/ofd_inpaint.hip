@@ -940,6 +940,8 @@ __device__ __forceinline__ void hole_wave_lds(const Chunk &ch, const uint32_t *_
     const int H = m.H, W = m.W, R = range, D = 2 * range + 1, npos = D * D;
     int64_t qe[2];
     unsigned hge[2];  // sample()'s test: hole of layer >= L
+    float vo0[2][kChanGroup], vi0[2][kChanGroup];  // first channel group, loaded with the flags
+    const int nc0 = min(kChanGroup, m.C);
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
         const int e = lane + 64 * u;
@@ -947,6 +949,14 @@ __device__ __forceinline__ void hole_wave_lds(const Chunk &ch, const uint32_t *_
         const bool inimg = k >= 0 && k < H && l >= 0 && l < W;
         const int kc = min(max(k, 0), H - 1), lc = min(max(l, 0), W - 1);
         qe[u] = int64_t(kc) * W + lc;
+#pragma unroll
+        for (int c = 0; c < kChanGroup; ++c) {
+            vo0[u][c] = vi0[u][c] = 0.f;
+            if (c < nc0 && e < kPatchN) {
+                vo0[u][c] = m.out[int64_t(c) * m.HW + qe[u]];
+                vi0[u][c] = m.img[int64_t(c) * m.HW + qe[u]];
+            }
+        }
         if (e < kPatchN) {
             const unsigned cd = m.code[qe[u]];
             const float tq = m.T[qe[u]];
@@ -983,12 +993,19 @@ __device__ __forceinline__ void hole_wave_lds(const Chunk &ch, const uint32_t *_
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             const int e = lane + 64 * u;
-            if (e < kPatchN)
-                for (int c = 0; c < nc; ++c) {
-                    const int cc = c0 + c;
-                    const float vo = m.out[int64_t(cc) * m.HW + qe[u]], vi = m.img[int64_t(cc) * m.HW + qe[u]];
-                    P.sv[c][e] = hge[u] ? int(to_u8(vi)) : int(vo);
+            if (e < kPatchN) {
+                if (c0 == 0) {
+#pragma unroll
+                    for (int c = 0; c < kChanGroup; ++c)
+                        if (c < nc) P.sv[c][e] = hge[u] ? int(to_u8(vi0[u][c])) : int(vo0[u][c]);
+                } else {
+                    for (int c = 0; c < nc; ++c) {
+                        const int cc = c0 + c;
+                        const float vo = m.out[int64_t(cc) * m.HW + qe[u]], vi = m.img[int64_t(cc) * m.HW + qe[u]];
+                        P.sv[c][e] = hge[u] ? int(to_u8(vi)) : int(vo);
+                    }
                 }
+            }
         }
         wave_lds_sync();
         float Ia[kChanGroup], Jx[kChanGroup], Jy[kChanGroup];
