@@ -5,8 +5,8 @@ The reference imports the CUDA extension ``fw_cuda`` at module load
 missing native build fails at import exactly like the reference would.
 """
 from opticalflowfromdepth_amd import _native
-from opticalflowfromdepth_amd.fw import FW
+from opticalflowfromdepth_amd.fw import FW, ForwardWarp, forward_warp
 
 _native.lib()
 
-__all__ = ["FW"]
+__all__ = ["FW", "ForwardWarp", "forward_warp"]

@@ -8,9 +8,19 @@ of 64 synthetic 768x1024 images with C=6 channels per image ([RGB, depth,
 Half the images carry a disparity flow, half an ego-motion flow (per-image
 seeds 12345+i, camera parameters broadcast from rank 0 over RCCL).
 
-Multi-GPU: one process per GPU (torchrun), each rank warps its own 64-image
-shard (weak scaling, no data-path collective); timing is barrier-bracketed and
-the max over ranks is taken.  Rank 0 prints ONE JSON line.
+Multi-GPU: one process per GPU, each rank warps its own 64-image shard (weak
+scaling, no data-path collective; the reference's --split/--split_id sharding,
+preprocess.py:540-547); timing is barrier-bracketed and the max over ranks is
+taken.  Rank 0 prints ONE JSON line.  ``python bench.py --gpus N`` with no
+torchrun environment starts the N ranks itself (a torch.distributed.run child
+process, launched before anything touches the GPU) and exits with the worst
+rank's status; under torchrun (WORLD_SIZE set) it is one rank.
+
+Besides the headline, rank 0 reports (after the timed steps, outside the
+driver's clock contract): BASELINE config 2 (480x640, B=32), the config-3
+hole-fill, the fused first-stage warps, the config-5 bf16 warp, and the CPU
+baselines of BASELINE.md §3 (the C loop, the torch-CPU scatter-min warp and
+the torch-CPU geometry flow) on this box's host cores.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
 """
@@ -20,6 +30,8 @@ import argparse
 import json
 import os
 import platform
+import socket
+import subprocess
 import sys
 import time
 
@@ -33,7 +45,7 @@ METRIC = "Mpix/s forward-warped (768×1024, B=64) + %HBM roofline, 1/2/4/8 MI355
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -43,7 +55,7 @@ def parse():
     ap.add_argument("--width", type=int, default=1024)
     ap.add_argument("--ego-fraction", type=float, default=0.5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline wall budget")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline wall budget (headline leg)")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
     ap.add_argument("--check", action="store_true", help="verify one image against the oracle")
     ap.add_argument("--engine", choices=["tile", "split", "atomic"], default="tile")
@@ -51,34 +63,134 @@ def parse():
     ap.add_argument("--hole-fill-steps", type=int, default=5)
     ap.add_argument("--no-fused", action="store_true", help="skip the fused disparity-warp phase")
     ap.add_argument("--no-bf16", action="store_true", help="skip the config-5 bf16 warp phase")
-    return ap.parse_args()
+    ap.add_argument("--no-config2", action="store_true", help="skip the config-2 (480x640, B=32) phase")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher / collective / timing skeleton only, on CPU with gloo (tests)")
+    return ap.parse_args(argv)
+
+
+# ---------------------------------------------------------------- launcher
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv) -> int:
+    """Start n ranks of this script as one torch.distributed.run child (never
+    an exec: nothing in this process has touched the GPU) and return the worst
+    exit status.  Each rank reads RANK / LOCAL_RANK / WORLD_SIZE from torchrun
+    and runs main() on cuda:LOCAL_RANK; rank 0 prints the JSON line."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL on this host driver)
+    env.setdefault("OMP_NUM_THREADS", str(max(1, min(16, (os.cpu_count() or 1) // max(n, 1)))))
+    return subprocess.call(cmd, env=env)
+
+
+# ---------------------------------------------------------------- helpers
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
+def timed_events(fn, steps, stream):
+    """Mean ms per call of fn over `steps` calls, HIP events on `stream`."""
+    fn()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    for a, b in ev:
+        a.record(stream)
+        fn()
+        b.record(stream)
+    torch.cuda.synchronize()
+    return sum(a.elapsed_time(b) for a, b in ev) / steps
+
+
+def sample_idx(B, n):
+    """n image indices of a B-image batch covering both flow kinds (first
+    half disparity, second half ego-motion)."""
+    n = min(n, B)
+    return list(range(n // 2)) + list(range(B - (n - n // 2), B))
 
 
 def cpu_baseline(obj, flow, depth, budget_s, threads):
-    """Oracle (C restatement of fw_cuda_kernel.cu:28-47 + fw.py:27-43, OpenMP
-    over (image, channel) planes like the reference's <<<B, C>>> grid), timed
-    on this box's host cores over a bounded sample of the same workload."""
-    from oracle import oracle  # test infrastructure: baseline leg only
-    n_img = min(8, obj.shape[0])
-    half = n_img // 2
-    B = obj.shape[0]
-    idx = list(range(half)) + list(range(B - (n_img - half), B))  # both flow kinds
-    o = obj[idx].cpu().numpy()
-    f = flow[idx].cpu().numpy()
-    d = depth[idx].cpu().numpy()
-    oracle.fw_flow(o[:1], f[:1], d[:1], nthreads=threads)  # warm (build + page-in)
+    """BASELINE.md §3 on this box's host cores, over a bounded sample of the
+    same workload (images of both flow kinds):
+      value      -- the C loop (oracle/fw_oracle.c: the serial raster loop of
+                    fw_cuda_kernel.cu:28-47 + fw.py:27-43, OpenMP over
+                    (image, channel) planes like the reference's <<<B, C>>> grid)
+      torch_cpu  -- the torch-CPU scatter_reduce('amin') warp (oracle/torch_cpu.py)
+                    and the torch-CPU geometry.py-equivalent depth -> flow
+                    (synth.disparity_flow / ego_motion_flow on CPU tensors)."""
+    from oracle import oracle, torch_cpu  # test infrastructure: baseline leg only
+    from opticalflowfromdepth_amd import synth
+    B, C, H, W = obj.shape
+    idx = sample_idx(B, 8)
+    n_img = len(idx)
+    o, f, d = obj[idx].cpu(), flow[idx].cpu(), depth[idx].cpu()
+    on, fn_, dn = o.numpy(), f.numpy(), d.numpy()
+    oracle.fw_flow(on[:1], fn_[:1], dn[:1], nthreads=threads)  # warm (build + page-in)
     reps, t0 = 0, time.perf_counter()
     while True:
-        oracle.fw_flow(o, f, d, nthreads=threads)
+        oracle.fw_flow(on, fn_, dn, nthreads=threads)
         reps += 1
         el = time.perf_counter() - t0
         if el >= budget_s:
             break
-    px = reps * n_img * o.shape[2] * o.shape[3]
-    return {"value": px / el / 1e6, "unit": "Mpix/s", "cores": threads, "kind": "port",
-            "sample": f"{n_img} images (of the {B}-image batch, both flow kinds) x {reps} reps, "
-                      f"C={o.shape[1]}, {o.shape[2]}x{o.shape[3]}, oracle/fw_oracle.c serial-per-plane "
-                      f"loop, {el:.1f} s wall on {platform.processor() or platform.machine()}"}
+    px = reps * n_img * H * W
+    loop = px / el / 1e6
+
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        torch_cpu.fw_flow_scatter(o[:1], f[:1], d[:1])
+        reps_t, t0 = 0, time.perf_counter()
+        while True:
+            torch_cpu.fw_flow_scatter(o, f, d)
+            reps_t += 1
+            el_t = time.perf_counter() - t0
+            if el_t >= budget_s / 2:
+                break
+        # flow synthesis on torch-CPU: the same images' depth -> flow (both kinds)
+        seeds = [12345 + i for i in idx]
+        s, T = synth.batch_camera_params(seeds)
+        h = n_img // 2
+
+        def flows():
+            synth.disparity_flow(d[:h].double(), s[:h])
+            synth.ego_motion_flow(d[h:].double(), T[h:])
+        flows()
+        reps_f, t0 = 0, time.perf_counter()
+        while True:
+            flows()
+            reps_f += 1
+            el_f = time.perf_counter() - t0
+            if el_f >= budget_s / 4:
+                break
+    finally:
+        torch.set_num_threads(prev)
+    warp_t = reps_t * n_img * H * W / el_t / 1e6
+    flow_t = reps_f * n_img * H * W / el_f / 1e6
+    return {"value": round(loop, 2), "unit": "Mpix/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
+            "sample": f"{n_img} images (of the {B}-image batch, both flow kinds) x {reps} reps, C={C}, "
+                      f"{H}x{W}, oracle/fw_oracle.c serial-per-plane loop, {el:.1f} s wall",
+            "torch_cpu": {"warp_scatter_amin_mpix_s": round(warp_t, 2),
+                          "flow_geometry_mpix_s": round(flow_t, 2),
+                          "flow_then_warp_mpix_s": round(1.0 / (1.0 / warp_t + 1.0 / flow_t), 2),
+                          "threads": threads,
+                          "sample": f"same {n_img} images: oracle/torch_cpu.py scatter_reduce('amin') warp "
+                                    f"x {reps_t} reps ({el_t:.1f} s); synth.disparity_flow / ego_motion_flow "
+                                    f"(geometry.py:17-67, preprocess.py:239-298) on float64 CPU depth "
+                                    f"x {reps_f} reps ({el_f:.1f} s)"}}
 
 
 def hole_fill_phase(out, valid, coll, steps, stream):
@@ -88,14 +200,9 @@ def hole_fill_phase(out, valid, coll, steps, stream):
     from opticalflowfromdepth_amd import ops
     rgb = (out[:, 0:3] * valid).contiguous()
     res = ops.inpaint(rgb, valid, coll)  # warm-up (workspace, code paging)
+    ms = timed_events(lambda: ops.inpaint(rgb, valid, coll), steps, stream)
+    res = ops.inpaint(rgb, valid, coll)
     torch.cuda.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
-    for s, e in ev:
-        s.record(stream)
-        res = ops.inpaint(rgb, valid, coll)
-        e.record(stream)
-    torch.cuda.synchronize()
-    ms = sum(s.elapsed_time(e) for s, e in ev) / steps
     B, _, H, W = rgb.shape
     px = B * H * W
     gbs = px * 28 / (ms / 1e3) / 1e9
@@ -103,10 +210,46 @@ def hole_fill_phase(out, valid, coll, steps, stream):
         "metric": "Mpix/s hole-filled (utils.inpaint, layered Telea r=3, same batch)",
         "value": round(px / (ms / 1e3) / 1e6, 1), "unit": "Mpix/s", "ms_per_step": round(ms, 3), "steps": steps,
         "hole_fraction": round(float((valid == 0).float().mean()), 4),
-        "roofline": {"bound": "latency (one launch per hole layer)", "achieved": round(gbs, 1),
+        "roofline": {"bound": "latency (dependent hole layers)", "achieved": round(gbs, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 5),
                      "algorithmic_bytes_per_px": 28},
         "parity": "bit-exact vs oracle/inpaint_oracle.c layered mode; cv2 Telea parity unpinned (no OpenCV)"}
+
+
+def hole_fill_cpu_baseline(rgb, valid, coll, gpu_res, budget_s, threads):
+    """The reference's hole-fill runs cv2.inpaint(TELEA) per image on the CPU
+    (utils.py:149); timed here as the sequential restatement of that algorithm
+    (oracle/inpaint_oracle.c), OpenMP over images, on a bounded sample.  The
+    same sample measures how far the GPU's layered fill sits from the
+    sequential (cv2-order) fill on this workload."""
+    import numpy as np
+    from oracle import oracle  # test infrastructure: baseline leg only
+    B = rgb.shape[0]
+    idx = sample_idx(B, max(threads, 1))
+    n = len(idx)
+    r, v, c = rgb[idx].cpu().numpy(), valid[idx].cpu().numpy(), coll[idx].cpu().numpy()
+    reps, t0 = 0, time.perf_counter()
+    seq = None
+    while True:
+        seq = oracle.inpaint(r, v, c, 3, layered=False, nthreads=threads)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    px = reps * n * r.shape[2] * r.shape[3]
+    g = gpu_res[idx].cpu().numpy()
+    hole = np.broadcast_to(oracle.inpaint_mask(v, c)[:, None] != 0, g.shape)
+    dif = np.abs(g.astype(np.int32) - seq.astype(np.int32))[hole]
+    div = {"hole_values": int(dif.size), "max_abs": int(dif.max()) if dif.size else 0,
+           "p99_abs": float(np.percentile(dif, 99)) if dif.size else 0.0,
+           "mean_abs": round(float(dif.mean()), 3) if dif.size else 0.0,
+           "frac_differing": round(float((dif != 0).mean()), 4) if dif.size else 0.0,
+           "frac_over_8": round(float((dif > 8).mean()), 4) if dif.size else 0.0,
+           "images": n}
+    return {"value": px / el / 1e6, "unit": "Mpix/s", "cores": threads, "kind": "port",
+            "sample": f"{n} warped images (of the {B}-image batch, both flow kinds) x {reps} reps, "
+                      f"{r.shape[2]}x{r.shape[3]} RGB, oracle/inpaint_oracle.c sequential Telea (cv2.inpaint "
+                      f"restatement), one image per thread, {el:.1f} s wall"}, div
 
 
 def fused_disparity_phase(B, H, W, steps, dev, stream):
@@ -126,19 +269,8 @@ def fused_disparity_phase(B, H, W, steps, dev, stream):
         flow = pp.Convert.disparity_to_flow(pp.Convert.depth_to_disparity(depth, s), random_sign=False)
         return forward_warp_flow(torch.cat((rgb, depth, flow * -1.0), 1), flow, depth)
 
-    def timed(fn):
-        fn()
-        torch.cuda.synchronize()
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
-        for a, b in ev:
-            a.record(stream)
-            fn()
-            b.record(stream)
-        torch.cuda.synchronize()
-        return sum(a.elapsed_time(b) for a, b in ev) / steps
-
-    ms = timed(lambda: warp_disparity(rgb, depth, s))
-    ms_unfused = timed(unfused)
+    ms = timed_events(lambda: warp_disparity(rgb, depth, s), steps, stream)
+    ms_unfused = timed_events(unfused, steps, stream)
     px = B * H * W
     gbs = px * 48 / (ms / 1e3) / 1e9
     return {"metric": "Mpix/s fused depth->disparity->flow->splat (preprocess.py:356-359), C=6 out",
@@ -168,21 +300,10 @@ def fused_ego_phase(B, H, W, steps, dev, stream):
         d32 = depth.float()
         return forward_warp_flow(torch.cat((rgb, d32, flow * -1.0), 1), flow, d32)
 
-    def timed(fn):
-        fn()
-        torch.cuda.synchronize()
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
-        for a, b in ev:
-            a.record(stream)
-            fn()
-            b.record(stream)
-        torch.cuda.synchronize()
-        return sum(a.elapsed_time(b) for a, b in ev) / steps
-
-    ms = timed(lambda: warp_ego(rgb, depth, P, ik))
-    ms_unfused = timed(unfused)
-    ms_flow = timed(lambda: ego_flow(depth, P, ik))
-    ms_flow_torch = timed(lambda: synth.ego_motion_flow(depth, T))
+    ms = timed_events(lambda: warp_ego(rgb, depth, P, ik), steps, stream)
+    ms_unfused = timed_events(unfused, steps, stream)
+    ms_flow = timed_events(lambda: ego_flow(depth, P, ik), steps, stream)
+    ms_flow_torch = timed_events(lambda: synth.ego_motion_flow(depth, T), steps, stream)
     px = B * H * W
     gbs = px * 52 / (ms / 1e3) / 1e9
     return {"metric": "Mpix/s fused depth->ego-motion flow->splat (preprocess.py:385-387), C=6 out",
@@ -206,20 +327,8 @@ def bf16_warp_phase(B, H, W, steps, dev, stream):
     C = obj.shape[1]
     outb = (torch.empty_like(objb), torch.empty_like(depth), torch.empty_like(depth))
     outf = (torch.empty_like(obj), torch.empty_like(depth), torch.empty_like(depth))
-
-    def timed(fn):
-        fn()
-        torch.cuda.synchronize()
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
-        for a, b in ev:
-            a.record(stream)
-            fn()
-            b.record(stream)
-        torch.cuda.synchronize()
-        return sum(a.elapsed_time(b) for a, b in ev) / steps
-
-    ms = timed(lambda: forward_warp_flow(objb, flow, depth, out=outb))
-    ms_f32 = timed(lambda: forward_warp_flow(obj, flow, depth, out=outf))
+    ms = timed_events(lambda: forward_warp_flow(objb, flow, depth, out=outb), steps, stream)
+    ms_f32 = timed_events(lambda: forward_warp_flow(obj, flow, depth, out=outf), steps, stream)
     same = bool(torch.equal(outb[0].view(torch.int16), outf[0].to(torch.bfloat16).view(torch.int16)))
     px = B * H * W
     bpp = 4 * C + 20
@@ -234,34 +343,96 @@ def bf16_warp_phase(B, H, W, steps, dev, stream):
             "parity": "bit-exact vs the oracle and the float32 path (tests/test_bf16.py)"}
 
 
-def hole_fill_cpu_baseline(rgb, valid, coll, budget_s, threads):
-    """The reference's hole-fill runs cv2.inpaint(TELEA) per image on the CPU
-    (utils.py:149); timed here as the sequential restatement of that algorithm
-    (oracle/inpaint_oracle.c), OpenMP over images, on a bounded sample."""
-    from oracle import oracle  # test infrastructure: baseline leg only
-    B = rgb.shape[0]
-    n = min(max(threads, 1), B)
-    idx = list(range(n // 2)) + list(range(B - (n - n // 2), B))  # both flow kinds
-    r, v, c = rgb[idx].cpu().numpy(), valid[idx].cpu().numpy(), coll[idx].cpu().numpy()
-    reps, t0 = 0, time.perf_counter()
-    while True:
-        oracle.inpaint(r, v, c, 3, layered=False, nthreads=threads)
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s:
-            break
-    px = reps * n * r.shape[2] * r.shape[3]
-    return {"value": px / el / 1e6, "unit": "Mpix/s", "cores": threads, "kind": "port",
-            "sample": f"{n} warped images (of the {B}-image batch, both flow kinds) x {reps} reps, 768x1024 RGB, "
-                      f"oracle/inpaint_oracle.c sequential Telea (cv2.inpaint restatement), one image per thread, "
-                      f"{el:.1f} s wall"}
+def config2_phase(steps, dev, stream, threads, cpu_budget):
+    """BASELINE config 2: 480x640, B=32, C=6, fp32 on one GPU (images 0-15
+    disparity flow, 16-31 ego-motion flow, seeds 12345+i; the
+    preprocess.py:358-359 / :385-387 call shape), with its roofline at 68 B/px
+    and its CPU baseline.  Parity is tests/test_configs.py (every image
+    bit-exact vs the oracle)."""
+    from opticalflowfromdepth_amd import _native, forward_warp_flow, synth
+    B, H, W = 32, 480, 640
+    seeds = [12345 + i for i in range(B)]
+    obj, flow, depth = synth.stage_one_batch(seeds, H, W, dev)
+    C = obj.shape[1]
+    out = (torch.empty_like(obj), torch.empty_like(depth), torch.empty_like(depth))
+    lib = _native.lib()
+    for _ in range(3):
+        forward_warp_flow(obj, flow, depth, out=out)
+    torch.cuda.synchronize()
+    ks = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    for a, b in ks:  # force the HIP event handles to exist
+        a.record(stream)
+        b.record(stream)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for a, b in ks:
+        lib.ofd_fw_set_profile_events(a.cuda_event, b.cuda_event)
+        forward_warp_flow(obj, flow, depth, out=out)
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / steps
+    lib.ofd_fw_set_profile_events(None, None)
+    kern_ms = sum(a.elapsed_time(b) for a, b in ks) / steps
+    px = B * H * W
+    bpp = (2 * C + 5) * 4
+    rec = {"metric": "Mpix/s forward-warped (480×640, B=32) + %HBM roofline, BASELINE config 2",
+           "value": round(px / wall / 1e6, 1), "unit": "Mpix/s", "ms_per_step": round(wall * 1e3, 4),
+           "steps": steps, "images": B, "height": H, "width": W, "channels": C, "dtype": "f32",
+           "roofline": {"bound": "hbm", "achieved": round(px * bpp / (kern_ms / 1e3) / 1e9, 1),
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(px * bpp / (kern_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                        "kernel": "splat_persist_kernel", "event_ms_per_launch": round(kern_ms, 4),
+                        "algorithmic_bytes_per_px": bpp},
+           "op_roofline": {"bound": "hbm", "achieved": round(px * bpp / wall / 1e9, 1), "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": round(px * bpp / wall / 1e9 / HBM_PEAK_GBS, 4),
+                           "scope": "whole call, wall clock"},
+           "parity": "every image bit-exact vs the oracle (tests/test_configs.py)"}
+    if cpu_budget > 0:
+        rec["cpu_baseline"] = cpu_baseline(obj, flow, depth, cpu_budget, threads)
+    return rec
 
 
-def main():
-    args = parse()
+# ---------------------------------------------------------------- main
+def dry_run(args, world, rank):
+    """The launcher / collective / timing skeleton without a GPU (tests): gloo
+    collectives, barrier-bracketed timing, max over ranks, one JSON line."""
+    if world > 1:
+        dist.init_process_group("gloo")
+    from opticalflowfromdepth_amd import shard
+    n_total = args.batch * world
+    seeds = [shard.image_seed(i) for i in range(n_total)]
+    s_all, _ = shard.broadcast_camera_params(seeds, device="cpu")
+    a, b = shard.shard_range(n_total, world, rank)
+    x = torch.zeros(b - a)
+    for _ in range(args.warmup):
+        x += 1
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        x += s_all[a:b]
+    if world > 1:
+        dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "Mpix/s", "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup, "dry_run": True,
+                          "shard_images": [a, b], "wall_s": float(t[0])}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, argv))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        return dry_run(args, world, rank)
     # OFD_BENCH_BACKEND=gloo + OFD_BENCH_SAME_DEVICE=1 rehearse the N>1 path on
     # a one-GPU box (all ranks on cuda:0, CPU collectives); the default is one
     # rank per GPU with RCCL ("nccl" on ROCm).
@@ -374,8 +545,13 @@ def main():
 
     cpu = None
     threads = args.cpu_threads if args.cpu_threads > 0 else min(16, os.cpu_count() or 1)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    cpu_on = rank == 0 and world == 1 and not args.no_cpu_baseline
+    if cpu_on:
         cpu = cpu_baseline(obj, flow, depth, args.cpu_seconds, threads)
+
+    cfg2 = None
+    if rank == 0 and not args.no_config2:
+        cfg2 = config2_phase(20, dev, stream, threads, args.cpu_seconds / 2 if cpu_on else 0)
 
     fused = fused_ego = None
     if rank == 0 and not args.no_fused:
@@ -388,9 +564,10 @@ def main():
 
     hole = None
     if rank == 0 and not args.no_hole_fill:  # untimed by the driver's clock contract: after the K steps
-        rgb, _, hole = hole_fill_phase(out[0], out[1], out[2], args.hole_fill_steps, stream)
-        if world == 1 and not args.no_cpu_baseline:
-            hole["cpu_baseline"] = hole_fill_cpu_baseline(rgb, out[1], out[2], args.cpu_seconds, threads)
+        rgb, res, hole = hole_fill_phase(out[0], out[1], out[2], args.hole_fill_steps, stream)
+        if cpu_on:
+            hole["cpu_baseline"], hole["divergence_vs_sequential"] = hole_fill_cpu_baseline(
+                rgb, out[1], out[2], res, args.cpu_seconds, threads)
 
     if rank == 0:
         rec = {
@@ -424,6 +601,7 @@ def main():
                             "algorithmic_bytes_per_px": bytes_per_px,
                             ("event_ms_per_call" if evmode >= 2 else "wall_ms_per_call"): round(dev_ms, 4)},
             "cpu_baseline": cpu,
+            "config2": cfg2,
             "hole_fill": hole,
             "fused_disparity": fused,
             "fused_ego": fused_ego,

@@ -40,7 +40,7 @@ size_t ofd_inpaint_workspace_bytes(int64_t B, int64_t H, int64_t W);
 /* utils.inpaint, batched.  img / out [B,C,H,W] f32 (out holds uint8 values),
  * valid / collision [B,1,H,W] f32.  radius = cv2 inpaintRange (3 in the
  * reference), clamped to [1, 100].  Requires H >= 2, W >= 2 (OFD_FW_EINVAL)
- * and H + W <= 8192 (OFD_FW_ETOOBIG).  out must not alias img. */
+ * and H + W <= 4096 (OFD_FW_ETOOBIG).  out must not alias img. */
 int ofd_inpaint_telea_f32(const float *img, const float *valid, const float *collision, float *out,
                           int64_t B, int64_t C, int64_t H, int64_t W, int radius, void *workspace,
                           size_t workspace_bytes, void *stream);

@@ -18,7 +18,7 @@ from torch import nn
 
 from . import ops
 
-__all__ = ["FW"]
+__all__ = ["FW", "ForwardWarp", "forward_warp"]
 
 
 class FW(nn.Module):
@@ -51,3 +51,27 @@ class FW(nn.Module):
         if not batched:
             output, valid, collision = output.squeeze(0), valid.squeeze(0), collision.squeeze(0)
         return output, valid, collision
+
+
+class ForwardWarp(torch.autograd.Function):
+    """``torch.autograd.Function`` form of FW.forward (BASELINE.json north_star:
+    "fw.forward_warp / torch.autograd.Function signature").  The reference
+    imports ``Function`` (alt_cuda/fw.py:3) but never defines one and FW has
+    no backward: a z-buffered splat selects a source per target, so there is
+    no gradient to give.  ``backward`` therefore raises; valid / collision are
+    marked non-differentiable."""
+
+    @staticmethod
+    def forward(ctx, obj, flow, depth):
+        output, valid, collision = FW()(obj, flow, depth)
+        ctx.mark_non_differentiable(valid, collision)
+        return output, valid, collision
+
+    @staticmethod
+    def backward(ctx, *grads):
+        raise NotImplementedError("forward warping has no backward (alt_cuda/fw.py defines none)")
+
+
+def forward_warp(obj: torch.Tensor, flow: torch.Tensor, depth: torch.Tensor):
+    """Functional FW: ``ForwardWarp.apply(obj, flow, depth) -> (output, valid, collision)``."""
+    return ForwardWarp.apply(obj, flow, depth)

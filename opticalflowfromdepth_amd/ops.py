@@ -22,7 +22,8 @@ There is no CPU path: the reference raises for non-GPU tensors
 from __future__ import annotations
 
 import threading
-from typing import Dict, List, Tuple
+from collections import OrderedDict
+from typing import List, Tuple
 
 import torch
 
@@ -30,12 +31,26 @@ from . import _native
 
 _F32, _F64, _BF16 = torch.float32, torch.float64, torch.bfloat16
 
-# Reusable key workspaces, one per (device, stream); each call leaves its
-# workspace in the initial all-ones state (see include/ofd_fw.h).
+# Reusable key workspaces, one per (device, stream) -- a workspace is
+# stream-ordered scratch, so two streams never share one; each call leaves its
+# workspace in the initial all-ones state (see include/ofd_fw.h).  The caches
+# are LRU-bounded: a caller that creates a stream per call or per worker
+# recycles workspaces instead of keeping one (~0.3-0.7 GB at 64 images of
+# 768x1024) per stream ever seen.  A dropped workspace was allocated on its
+# stream, so the caching allocator hands its memory out again only in that
+# stream's order.
 _ws_lock = threading.Lock()
-_workspaces: Dict[Tuple[int, int], torch.Tensor] = {}
+_WS_CACHE_MAX = 4
+_workspaces: "OrderedDict[Tuple[int, int], torch.Tensor]" = OrderedDict()
 # hole-fill scratch, one per (device, stream); needs no initialisation
-_ip_workspaces: Dict[Tuple[int, int], torch.Tensor] = {}
+_ip_workspaces: "OrderedDict[Tuple[int, int], torch.Tensor]" = OrderedDict()
+
+
+def _cache_put(cache: OrderedDict, key, ws: torch.Tensor) -> None:
+    cache[key] = ws
+    cache.move_to_end(key)
+    while len(cache) > _WS_CACHE_MAX:
+        cache.popitem(last=False)
 
 
 def _check_input(x: torch.Tensor, name: str) -> None:
@@ -54,16 +69,29 @@ def workspace(device: torch.device, nbytes: int, stream: torch.cuda.Stream) -> t
     with _ws_lock:
         ws = _workspaces.get(key)
         if ws is None or ws.numel() < nbytes:
+            _workspaces.pop(key, None)  # release the smaller one before allocating
+            ws = None
             with torch.cuda.device(device), torch.cuda.stream(stream):
                 ws = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=device)
             _native.check(_native.lib().ofd_fw_workspace_init(ws.data_ptr(), ws.numel(), stream.cuda_stream),
                           "ofd_fw_workspace_init")
-            _workspaces[key] = ws
+        _cache_put(_workspaces, key, ws)
         return ws
 
 
 def _ws_bytes(B: int, H: int, W: int, f64: bool) -> int:
     return int(_native.lib().ofd_fw_workspace_bytes(B, H, W, 1 if f64 else 0))
+
+
+def _check_out(out, shapes, dtypes, dev):
+    """Validate caller-supplied (output, valid, collision) like forward_warp_flow does."""
+    if len(out) != 3:
+        raise RuntimeError("out must be (output, valid, collision)")
+    for x, n, shp, dt in zip(out, ("output", "valid", "collision"), shapes, dtypes):
+        _check_input(x, n)
+        if tuple(x.shape) != tuple(shp) or x.dtype != dt or x.device != dev:
+            raise RuntimeError(f"out {n} must be {dt} {tuple(shp)} on {dev}")
+    return out
 
 
 def forward_warping(obj: torch.Tensor, safe_y: torch.Tensor, safe_x: torch.Tensor,
@@ -148,13 +176,8 @@ def forward_warp_flow(obj: torch.Tensor, flow: torch.Tensor, depth: torch.Tensor
             valid = torch.empty_like(depth)
             collision = torch.empty_like(depth)
         else:
-            output, valid, collision = out
-            for x, n, shp in ((output, "output", (B, C, H, W)), (valid, "valid", (B, 1, H, W)),
-                              (collision, "collision", (B, 1, H, W))):
-                _check_input(x, n)
-                dt = obj.dtype if n == "output" else _F32
-                if tuple(x.shape) != shp or x.dtype != dt or x.device != dev:
-                    raise RuntimeError(f"out {n} must be {dt} {shp} on {dev}")
+            output, valid, collision = _check_out(out, ((B, C, H, W), (B, 1, H, W), (B, 1, H, W)),
+                                                  (obj.dtype, _F32, _F32), dev)
         nbytes = _ws_bytes(B, H, W, False)
         ws = workspace(dev, nbytes, stream) if nbytes else None
         lib = _native.lib()
@@ -209,8 +232,11 @@ def inpaint(img: torch.Tensor, valid: torch.Tensor, collision: torch.Tensor, rad
             with _ws_lock:
                 ws = _ip_workspaces.get(key)
                 if ws is None or ws.numel() < nbytes:
-                    ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-                    _ip_workspaces[key] = ws
+                    _ip_workspaces.pop(key, None)
+                    ws = None
+                    with torch.cuda.stream(stream):
+                        ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+                _cache_put(_ip_workspaces, key, ws)
         rc = lib.ofd_inpaint_telea_f32(img.data_ptr(), valid.data_ptr(), collision.data_ptr(), out.data_ptr(),
                                        B, C, H, W, int(radius),
                                        ws.data_ptr() if ws is not None else None,
@@ -256,7 +282,8 @@ def warp_disparity(obj: torch.Tensor, depth: torch.Tensor, s: torch.Tensor,
             valid = torch.empty(B, 1, H, W, dtype=_F32, device=dev)
             collision = torch.empty_like(valid)
         else:
-            output, valid, collision = out
+            output, valid, collision = _check_out(out, ((B, Cobj + 3, H, W), (B, 1, H, W), (B, 1, H, W)),
+                                                  (_F32, _F32, _F32), dev)
         nbytes = _ws_bytes(B, H, W, False)
         ws = workspace(dev, nbytes, stream) if nbytes else None
         lib = _native.lib()
@@ -335,7 +362,8 @@ def warp_ego(obj: torch.Tensor, depth: torch.Tensor, P: torch.Tensor, inv_K: tor
             valid = torch.empty(B, 1, H, W, dtype=_F32, device=dev)
             collision = torch.empty_like(valid)
         else:
-            output, valid, collision = out
+            output, valid, collision = _check_out(out, ((B, Cobj + 3, H, W), (B, 1, H, W), (B, 1, H, W)),
+                                                  (_F32, _F32, _F32), dev)
         nbytes = _ws_bytes(B, H, W, False)
         ws = workspace(dev, nbytes, stream) if nbytes else None
         lib = _native.lib()

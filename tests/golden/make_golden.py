@@ -386,12 +386,54 @@ def make_inpaint_mask_cases(ref_inpaint, rec):
     return cases
 
 
+def _digest(a) -> str:
+    import hashlib
+    a = np.ascontiguousarray(a)
+    return f"{a.dtype.str}{tuple(a.shape)}:" + hashlib.sha256(a.tobytes()).hexdigest()
+
+
+def make_config1_cases(ref_fw, Convert, utils_mod):
+    """BASELINE config 1: one 480x640 synthetic depth map (seed
+    0) through the reference's normalize_depth (utils.py:102-116), its
+    disparity flow (preprocess.py:239-254, s drawn after utils.set_seed(12345))
+    and ego-motion flow (:265-298 with geometry.py, the next draws), each
+    warped by the reference's fw.py (oracle as fw_cuda) with the :358 / :386
+    obj.  Full planes at this size would be megabytes, so the fixture holds a
+    SHA-256 digest of every array plus a strided sample of its values (for
+    readable failures) and the scalar draws."""
+    h, w = 480, 640
+    fw = ref_fw.FW("cpu")
+    raw = synth_depth(h, w, 0)
+    rgb = torch.from_numpy(synth_rgb(h, w, 0))
+    utils_mod.set_seed(12345)
+    d0 = utils_mod.normalize_depth(torch.from_numpy(raw.copy()).unsqueeze(0))   # float64 (utils.get_depth)
+    flow01 = Convert.disparity_to_flow(Convert.depth_to_disparity(d0), device="cpu", random_sign=False)
+    o1, v1, c1 = fw(torch.cat((rgb, d0, flow01 * -1.0), 0), flow01, d0)          # preprocess.py:358-359
+    d0f = d0.to(torch.float32)
+    flow03, T1 = Convert.depth_to_random_flow(d0f, "cpu")                         # preprocess.py:372 / :385
+    o3, v3, c3 = fw(torch.cat((rgb, d0f, flow03 * -1.0), 0), flow03, d0f)        # preprocess.py:386-387
+    arrays = {"raw_depth": raw, "rgb": rgb.numpy(), "norm_depth": d0.numpy(), "flow01": flow01.numpy(),
+              "fw01_output": o1.numpy(), "fw01_valid": v1.numpy(), "fw01_collision": c1.numpy(),
+              "flow03": flow03.numpy(), "fw03_output": o3.numpy(), "fw03_valid": v3.numpy(),
+              "fw03_collision": c3.numpy()}
+    cases = {"T1": T1.numpy()}
+    for k, a in arrays.items():
+        cases[f"digest/{k}"] = np.array(_digest(a))
+        cases[f"sample/{k}"] = np.ascontiguousarray(a).reshape(-1)[::97].copy()
+    return cases
+
+
 def main():
     ref_fw = load_reference_fw()
     geometry_mod = load_reference_geometry()
     utils_mod = load_reference_utils_subset()
     Plausible, Convert = load_reference_plausible_convert(utils_mod, geometry_mod)
 
+    if sys.argv[1:] == ["config1"]:  # only the config-1 fixture (the others are unchanged)
+        c1 = make_config1_cases(ref_fw, Convert, utils_mod)
+        np.savez_compressed(os.path.join(HERE, "config1.npz"), **c1)
+        print("config1.npz", os.path.getsize(os.path.join(HERE, "config1.npz")), "bytes")
+        return
     op = make_op_cases()
     np.savez_compressed(os.path.join(HERE, "fw_op.npz"), **op)
     wr = make_wrapper_cases(ref_fw)

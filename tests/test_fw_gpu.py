@@ -270,6 +270,36 @@ def test_FW_3d_matches_batched(cuda_device):
         assert torch.equal(o, ob[i]) and torch.equal(v, vb[i]) and torch.equal(c, cb[i])
 
 
+def test_forward_warp_autograd_function(cuda_device):
+    """alt_cuda.fw.forward_warp (the autograd.Function form) == FW; no backward."""
+    import alt_cuda.fw as afw
+    from opticalflowfromdepth_amd import synth
+    obj, flow, depth = synth.stage_one_batch([3, 4], 40, 56, cuda_device)
+    a = afw.FW()(obj, flow, depth)
+    b = afw.forward_warp(obj, flow, depth)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+    o, v, c = afw.forward_warp(obj.clone().requires_grad_(True), flow, depth)
+    assert o.requires_grad and not v.requires_grad and not c.requires_grad
+    with pytest.raises(NotImplementedError):
+        o.sum().backward()
+
+
+def test_fused_out_validation(cuda_device):
+    from opticalflowfromdepth_amd import synth, warp_disparity
+    seeds = [1, 2]
+    depth = synth.normalize_depth(synth.synthetic_depth(seeds, 32, 48, cuda_device))
+    rgb = synth.synthetic_rgb(seeds, 32, 48, cuda_device)
+    s = torch.ones(2)
+    good = (torch.empty(2, 6, 32, 48, device=cuda_device), torch.empty(2, 1, 32, 48, device=cuda_device),
+            torch.empty(2, 1, 32, 48, device=cuda_device))
+    warp_disparity(rgb, depth, s, out=good)
+    with pytest.raises(RuntimeError, match="out output"):
+        warp_disparity(rgb, depth, s, out=(good[0][:, :5].contiguous(), good[1], good[2]))
+    with pytest.raises(RuntimeError, match="out valid"):
+        warp_disparity(rgb, depth, s, out=(good[0], good[1].double(), good[2]))
+
+
 # ------------------------------------------------------------------ every engine
 # 0 = TILE (fused SPLAT gathers the output), 1 = ATOMIC, 2 = TILE_SPLIT (winner map + RESOLVE)
 @pytest.fixture(params=[1, 2], ids=["atomic", "split"])

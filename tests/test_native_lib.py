@@ -113,6 +113,32 @@ def test_drop_in_module_surface():
     assert isinstance(m, torch.nn.Module) and m.device == "cuda:0"
     assert list(m.parameters()) == [] and list(m.buffers()) == []
     assert callable(fw_cuda.forward_warping)
+    # the autograd.Function form named by the north star (fw.forward_warp)
+    assert issubclass(afw.ForwardWarp, torch.autograd.Function)
+    assert callable(afw.forward_warp)
+    with pytest.raises(RuntimeError, match="must be a CUDA tensor"):
+        afw.forward_warp(torch.zeros(3, 2, 2), torch.zeros(2, 2, 2), torch.zeros(1, 2, 2))
+
+
+def test_out_buffers_are_validated():
+    """Caller-supplied outputs of the fused warps are checked before the native
+    call writes through their pointers."""
+    from opticalflowfromdepth_amd import ops
+    t = torch.zeros(1, 3, 2, 2)
+    with pytest.raises(RuntimeError, match="CUDA tensor"):
+        ops._check_out((t, t[:, :1], t[:, :1]), ((1, 3, 2, 2), (1, 1, 2, 2), (1, 1, 2, 2)),
+                       (torch.float32,) * 3, torch.device("cpu"))
+    with pytest.raises(RuntimeError, match="out must be"):
+        ops._check_out((t,), (), (), torch.device("cpu"))
+
+
+def test_workspace_cache_is_bounded():
+    from opticalflowfromdepth_amd import ops
+    from collections import OrderedDict
+    c = OrderedDict()
+    for k in range(10):
+        ops._cache_put(c, (0, k), torch.zeros(1))
+    assert list(c) == [(0, k) for k in range(10 - ops._WS_CACHE_MAX, 10)]
 
 
 def test_product_never_imports_oracle():
