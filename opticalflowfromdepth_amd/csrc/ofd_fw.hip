@@ -103,6 +103,14 @@ __device__ __forceinline__ unsigned long long make_key(float d, unsigned int src
     return (d < 1000.0f) ? ((unsigned long long)orderable32(d) << 32) | src : KEY_NOWIN;
 }
 
+// The float32 depth a winning key carries: the inverse of orderable32 for
+// keys below KEY_NOWIN.  -0 was folded onto +0, so a decoded 0 is ambiguous
+// and the caller re-reads the depth plane for it.
+__device__ __forceinline__ float depth_from_key(unsigned long long key) {
+    const unsigned o = unsigned(key >> 32);
+    return __uint_as_float((o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o);
+}
+
 // ---------------------------------------------------------------- target maps
 // Op level: coordinates as given to fw_cuda.forward_warping.  The reference
 // indexes its accessor with them, i.e. converts float -> int32 by truncation
@@ -146,6 +154,16 @@ __device__ __forceinline__ void load4(const T *__restrict__ q, T v[4], int n) {
     }
 }
 
+// BIN's target range of one source: the exact target (lo == hi) for every
+// coordinate source except the ego-motion one (EgoCoords::target_range).
+#define TARGET_RANGE_EXACT                                                                              \
+    __device__ __forceinline__ void target_range(int64_t b, int i, int j, V x, V y, int H_, int W_, int &tx0, \
+                                                 int &tx1, int &ty0, int &ty1) const {                 \
+        target(b, i, j, x, y, H_, W_, tx0, ty0);                                                      \
+        tx1 = tx0;                                                                                    \
+        ty1 = ty0;                                                                                    \
+    }
+
 // Coordinate sources whose z-test depth is the separate float32 depth plane
 // and that generate no obj channels.
 #define KEY_DEPTH_FROM_PLANE                                                                            \
@@ -159,7 +177,8 @@ __device__ __forceinline__ void load4(const T *__restrict__ q, T v[4], int n) {
     __device__ __forceinline__ float key_depth(int64_t b, int64_t p, const float *depth) const {     \
         return depth[b * HW + p];                                                                     \
     }                                                                                                 \
-    __device__ __forceinline__ void gen_all(int64_t, unsigned, float *) const {}
+    __device__ __forceinline__ void gen_key(int64_t, unsigned, unsigned long long, float *) const {}      \
+    TARGET_RANGE_EXACT
 
 // Coordinate sources: the target of the source at pixel p = j*W + i of image b.
 struct SafeF32 {  // fw_cuda.forward_warping inputs: safe_y, safe_x [B,1,H,W]
@@ -215,7 +234,7 @@ struct FlowCoords {  // FW.forward input: flow [B,2,H,W], ch0 = x, ch1 = y
 template <typename D>
 struct DisparityCoords {
     using V = D;
-    static constexpr int kGen = 3, kGenGT = 4;
+    static constexpr int kGen = 3, kGenGT = 8;
     const D *depth;
     const float *s;  // [B] per-image scale
     int64_t HW;
@@ -249,9 +268,19 @@ struct DisparityCoords {
     __device__ __forceinline__ float key_depth(int64_t b, int64_t p, const float *) const {
         return float(depth[b * HW + p]);
     }
-    // generated obj channels of source w: depth, flow_x * -1.0 = disparity, flow_y * -1.0 = +0
-    __device__ __forceinline__ void gen_all(int64_t b, unsigned w, float g[3]) const {
-        const D d = depth[b * HW + w];
+    // The winner's depth: a float32 depth is the key's high half (no gather);
+    // a float64 depth is re-read (the key holds only its float32 rounding).
+    __device__ __forceinline__ D winner_depth(int64_t b, unsigned w, unsigned long long key) const {
+        if constexpr (std::is_same<D, float>::value) {
+            const float d = depth_from_key(key);
+            return d != 0.0f ? d : depth[b * HW + w];
+        } else {
+            return depth[b * HW + w];
+        }
+    }
+    // generated obj channels of winner w: depth, flow_x * -1.0 = disparity, flow_y * -1.0 = +0
+    __device__ __forceinline__ void gen_key(int64_t b, unsigned w, unsigned long long key, float g[3]) const {
+        const D d = winner_depth(b, w, key);
         g[0] = float(d);
         g[1] = float(disp(b, d));
         g[2] = 0.0f;
@@ -260,6 +289,7 @@ struct DisparityCoords {
     __device__ __forceinline__ void target(int64_t, int i, int j, V x, V y, int H, int W, int &tx, int &ty) const {
         target_flow<D>(i, j, x, y, H, W, tx, ty);
     }
+    TARGET_RANGE_EXACT
 };
 
 // Ego-motion flow (Convert.depth_to_random_flow, preprocess.py:265-298, with
@@ -281,9 +311,13 @@ struct EgoCam {
     float ik[9];  // inv_K[:3,:3], row-major (the same for every image)
 };
 
-template <typename D>
+// kApprox: the four divisions become multiplications by v_rcp_f32 (1 ulp);
+// every other operation is the exact sequence's.  Only BIN's conservative
+// target-tile boxes use it (ego_box_range), never a published value.
+template <typename D, bool kApprox = false>
 __device__ __forceinline__ void ego_flow_at(const EgoCam &cam, const float *__restrict__ Pb, int i, int j, D d,
                                             int H, int W, float &fx, float &fy) {
+    auto dv = [](float a, float b) -> float { return kApprox ? a * __builtin_amdgcn_rcpf(b) : a / b; };
     const float x = float(i), y = float(j);
     float c[3];
 #pragma unroll
@@ -296,9 +330,9 @@ __device__ __forceinline__ void ego_flow_at(const EgoCam &cam, const float *__re
     for (int k = 0; k < 3; ++k)
         cp[k] = fmaf(Pb[4 * k + 3], 1.0f, fmaf(Pb[4 * k + 2], X[2], fmaf(Pb[4 * k + 1], X[1], Pb[4 * k] * X[0])));
     const float den = cp[2] + 1e-7f;
-    float u = cp[0] / den, v = cp[1] / den;
-    u = u / float(W - 1);
-    v = v / float(H - 1);
+    float u = dv(cp[0], den), v = dv(cp[1], den);
+    u = dv(u, float(W - 1));
+    v = dv(v, float(H - 1));
     u = (u - 0.5f) * 2.0f;
     v = (v - 0.5f) * 2.0f;
     u = (u + 1.0f) / 2.0f;
@@ -307,6 +341,22 @@ __device__ __forceinline__ void ego_flow_at(const EgoCam &cam, const float *__re
     v = v * float(H - 1);
     fx = u - x;
     fy = v - y;
+}
+
+// [lo, hi] bounds on trunc(clamp(p_exact, 0, n - 1)) from the approximate
+// coordinate p (= i + fx of ego_flow_at<D, true>).  Replacing the four
+// divisions by v_rcp_f32 products moves p by at most
+// 2^-24 * (~20 |p| + ~3.2 n) (rcp 1 ulp, each later rounding 1/2 ulp, the
+// normalise / denormalise steps scaling the error by n - 1); the margin
+// 32 * 2^-24 * (|p| + n + 1) covers it.  false: p is not finite (NaN depth,
+// a zero denominator) -- the caller takes the exact target.
+__device__ __forceinline__ bool approx_trunc_range(float p, int n, int &lo, int &hi) {
+    if (!(fabsf(p) < 1.0e30f)) return false;
+    const float m = 1.9073486328125e-06f * (fabsf(p) + float(n) + 1.0f);
+    const float a = fminf(fmaxf(p - m, 0.0f), float(n - 1)), b = fminf(fmaxf(p + m, 0.0f), float(n - 1));
+    lo = int(a);
+    hi = int(b);
+    return true;
 }
 
 // Fused depth -> ego-motion flow -> splat: the flow is derived from the depth
@@ -318,7 +368,7 @@ struct EgoCoords {
     // the flow is computed in target(), after every load of a batch of
     // sources has been issued, which keeps SPLAT's loads in flight together.
     using V = D;
-    static constexpr int kGen = 3, kGenGT = 2;
+    static constexpr int kGen = 3, kGenGT = 4;
     const D *depth;
     const float *P;  // [B][3][4] float32 (K @ T)[:3]
     EgoCam cam;
@@ -352,9 +402,17 @@ struct EgoCoords {
     __device__ __forceinline__ float key_depth(int64_t b, int64_t p, const float *) const {
         return float(depth[b * HW + p]);
     }
-    // generated obj channels of source w: depth, flow_x * -1.0, flow_y * -1.0
-    __device__ __forceinline__ void gen_all(int64_t b, unsigned w, float g[3]) const {
-        const D d = depth[b * HW + w];
+    __device__ __forceinline__ D winner_depth(int64_t b, unsigned w, unsigned long long key) const {
+        if constexpr (std::is_same<D, float>::value) {
+            const float d = depth_from_key(key);
+            return d != 0.0f ? d : depth[b * HW + w];
+        } else {
+            return depth[b * HW + w];
+        }
+    }
+    // generated obj channels of winner w: depth, flow_x * -1.0, flow_y * -1.0
+    __device__ __forceinline__ void gen_key(int64_t b, unsigned w, unsigned long long key, float g[3]) const {
+        const D d = winner_depth(b, w, key);
         const unsigned j = w / unsigned(W), i = w - j * unsigned(W);
         float fx, fy;
         ego_flow_at<D>(cam, Pof(b), int(i), int(j), d, H, W, fx, fy);
@@ -368,6 +426,19 @@ struct EgoCoords {
         float fx, fy;
         ego_flow_at<D>(cam, Pof(b), i, j, d, H, W, fx, fy);
         target_flow<float>(i, j, fx, fy, H_, W_, tx, ty);
+    }
+    // BIN's boxes only need a superset of the target tiles: the approximate
+    // flow widened by its error bound (approx_trunc_range), exact only where
+    // the approximation is not finite.
+    __device__ __forceinline__ void target_range(int64_t b, int i, int j, V d, V y, int H_, int W_, int &tx0,
+                                                 int &tx1, int &ty0, int &ty1) const {
+        float fx, fy;
+        ego_flow_at<D, true>(cam, Pof(b), i, j, d, H, W, fx, fy);
+        if (!approx_trunc_range(float(i) + fx, W_, tx0, tx1) || !approx_trunc_range(float(j) + fy, H_, ty0, ty1)) {
+            target(b, i, j, d, y, H_, W_, tx0, ty0);
+            tx1 = tx0;
+            ty1 = ty0;
+        }
     }
 };
 
@@ -583,12 +654,11 @@ __device__ __forceinline__ void bin_segment(const Coords &co, const float *__res
         const int j = jh + 2 * q;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            int tx = -1, ty = -1;
-            if (i0 + e < W && j < H) co.target(b, i0 + e, j, x[q][e], y[q][e], H, W, tx, ty);
-            if (tx >= 0) {
-                const unsigned ttx = unsigned(tx / TW), tty = unsigned(ty / TH);
-                mn = pk_min_u16(mn, ttx | (tty << 16));
-                mxi = pk_min_u16(mxi, (0xFFFFu - ttx) | ((0xFFFFu - tty) << 16));
+            int tx0 = -1, tx1 = -1, ty0 = -1, ty1 = -1;
+            if (i0 + e < W && j < H) co.target_range(b, i0 + e, j, x[q][e], y[q][e], H, W, tx0, tx1, ty0, ty1);
+            if (tx0 >= 0) {
+                mn = pk_min_u16(mn, unsigned(tx0 / TW) | (unsigned(ty0 / TH) << 16));
+                mxi = pk_min_u16(mxi, (0xFFFFu - unsigned(tx1 / TW)) | ((0xFFFFu - unsigned(ty1 / TH)) << 16));
             }
         }
     }
@@ -869,29 +939,82 @@ __device__ __forceinline__ void splat_tile(TileLds &L, unsigned lin, const Coord
     // ---- 5. publish (lane-consecutive rows of the tile)
     float *vb = io.valid + b * HW;
     float *cb = io.coll + b * HW;
-    if constexpr (kFuse) {
+    if constexpr (kFuse && Coords::kGen > 0) {
+        // Coordinate sources that generate obj channels (fused first-stage
+        // warps): the Cobj obj channels are gathered for kT targets at once,
+        // the kGen generated ones (depth, flow * -1.0) are computed once per
+        // target from the winner's depth -- the key's high half for a float32
+        // depth -- while those gathers are in flight.  Output channel c is
+        // obj channel c below gen_at, generated c - gen_at, then obj c - kGen.
+        constexpr int kT = Cfg::kGT, kCh = 4, kG = Coords::kGen;
+        const int C = io.C, Cobj = io.Cobj, ga = io.gen_at;
+        const float *ob = static_cast<const float *>(io.obj) + b * int64_t(Cobj) * HW;
+        float *oo = static_cast<float *>(io.out) + b * int64_t(C) * HW;
+        const unsigned uHW = unsigned(HW);
+#pragma unroll
+        for (int k = 0; k < TW * TH / Cfg::kThr; k += kT) {
+            unsigned t[kT], w[kT];
+            unsigned long long kk[kT];
+            bool in[kT];
+#pragma unroll
+            for (int u = 0; u < kT; ++u) {
+                const int q = int(threadIdx.x) + (k + u) * Cfg::kThr;
+                const int ly = q / TW, lx = q - ly * TW;
+                const int ty = y0 + ly, tx = x0 + lx;
+                in[u] = ty < H && tx < W;
+                kk[u] = L.zk[q];
+                const bool touched = kk[u] != KEY_UNTOUCHED;
+                const bool nowin = kk[u] == KEY_NOWIN;
+                t[u] = unsigned(ty) * unsigned(W) + unsigned(tx);
+                w[u] = (in[u] && touched && !nowin) ? unsigned(kk[u] & 0xFFFFFFFFull) : WIN_NONE;
+                if (in[u]) {
+                    __builtin_nontemporal_store(touched ? 1.f : 0.f, vb + t[u]);
+                    __builtin_nontemporal_store(nowin ? 1.f : 0.f, cb + t[u]);
+                }
+            }
+            for (int c0 = 0; c0 < (Cobj > 0 ? Cobj : 1); c0 += kCh) {
+                float o[kT][kCh];
+#pragma unroll
+                for (int u = 0; u < kT; ++u)
+#pragma unroll
+                    for (int cc = 0; cc < kCh; ++cc)
+                        o[u][cc] = (w[u] != WIN_NONE && c0 + cc < Cobj) ? ob[unsigned(c0 + cc) * uHW + w[u]] : 0.f;
+                if (c0 == 0) {  // the generated channels, computed while the first gathers fly
+#pragma unroll
+                    for (int u = 0; u < kT; ++u) {
+                        float g[kG];
+#pragma unroll
+                        for (int e = 0; e < kG; ++e) g[e] = 0.f;
+                        if (w[u] != WIN_NONE) co.gen_key(b, w[u], kk[u], g);
+                        if (in[u])
+#pragma unroll
+                            for (int e = 0; e < kG; ++e)
+                                __builtin_nontemporal_store(g[e], oo + unsigned(ga + e) * uHW + t[u]);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < kT; ++u)
+#pragma unroll
+                    for (int cc = 0; cc < kCh; ++cc) {
+                        const int c = c0 + cc;
+                        if (in[u] && c < Cobj)
+                            __builtin_nontemporal_store(o[u][cc], oo + unsigned(c < ga ? c : c + kG) * uHW + t[u]);
+                    }
+            }
+        }
+    } else if constexpr (kFuse) {
         // valid, collision, and the winners' C channels: kT targets per thread
         // with all their gathers in flight before any store.  The output
         // planes and masks are touched once: non-temporal.
         // E = unsigned short: bf16 planes moved as raw bits (the warp only
         // selects a source value, so no rounding happens anywhere)
-        static_assert(std::is_same<E, float>::value || Coords::kGen == 0, "generated channels are float32");
+        static_assert(Coords::kGen == 0, "generated channels take the branch above");
         constexpr int kT = Cfg::kGT, kCh = 8;
         const int C = io.C;
         const E *ob = static_cast<const E *>(io.obj) + b * int64_t(io.Cobj) * HW;
         E *oo = static_cast<E *>(io.out) + b * int64_t(C) * HW;
         const unsigned uHW = unsigned(HW);
-        auto source = [&](int c, unsigned wi) -> E {
-            if constexpr (Coords::kGen == 0) {
-                return ob[unsigned(c) * uHW + wi];
-            } else {
-                if (c < io.gen_at) return ob[unsigned(c) * uHW + wi];
-                float g[3];
-                co.gen_all(b, wi, g);
-                if (c < io.gen_at + Coords::kGen) return c == io.gen_at ? g[0] : (c == io.gen_at + 1 ? g[1] : g[2]);
-                return ob[unsigned(c - Coords::kGen) * uHW + wi];
-            }
-        };
+        auto source = [&](int c, unsigned wi) -> E { return ob[unsigned(c) * uHW + wi]; };
 #pragma unroll
         for (int k = 0; k < TW * TH / Cfg::kThr; k += kT) {
             unsigned t[kT], w[kT];

@@ -25,7 +25,7 @@ extern "C" int probe_launch(int which, const float *obj, const float *flow, cons
     using Co = FlowCoords<float>;
     Co co{flow, HW};
     const ChunkArgs a{carve(slab, nimg, HW, g), b0, nimg};
-    const SplatIO io{valid, coll, obj, out, int(C)};
+    const SplatIO io{valid, coll, obj, out, int(C), int(C), int(C)};  // Cobj = C, no generated channels
     hipStream_t st = static_cast<hipStream_t>(stream);
     const dim3 sgrid((unsigned(nimg * g.ntiles) + 7u) / 8u * 8u), blk(kWarpThreads);
     const int64_t nsg = int64_t(nimg) * g.nseg;
