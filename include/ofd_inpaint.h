@@ -22,6 +22,17 @@
  *   ofd_inpaint_workspace_bytes
  *       no reference counterpart (cv2 allocates its fast-marching state per
  *       call); caller-owned scratch, no initialisation needed.
+ *   ofd_inpaint_set_schedule
+ *       no reference counterpart: diagnostics / tests only (how many hole
+ *       layers are launched one by one before the persistent deep-tail kernel
+ *       takes over, and the layer size below which every hole takes the
+ *       wave-per-hole path).  Results never depend on it.
+ *
+ * The call never blocks the host: every launch reads its layer's size from
+ * the device.  The host sizes grids and the number of per-layer launches from
+ * the layer histogram of an earlier call at the same shape, read back
+ * asynchronously (pinned memory + event, used once it has arrived); layers
+ * beyond those launches run in one persistent kernel with grid barriers.
  */
 #ifndef OFD_INPAINT_H
 #define OFD_INPAINT_H
@@ -44,6 +55,13 @@ size_t ofd_inpaint_workspace_bytes(int64_t B, int64_t H, int64_t W);
 int ofd_inpaint_telea_f32(const float *img, const float *valid, const float *collision, float *out,
                           int64_t B, int64_t C, int64_t H, int64_t W, int radius, void *workspace,
                           size_t workspace_bytes, void *stream);
+
+/* Diagnostics: launch_layers >= 0 launches exactly that many hole layers one
+ * by one (the deep-tail kernel does the rest); thin_cap >= 0 sets the layer
+ * size up to which every hole takes the wave path.  -1 restores the
+ * defaults (launches sized from an earlier call's depth; thin_cap 4096).
+ * Process-wide; returns 0. */
+int ofd_inpaint_set_schedule(int launch_layers, int thin_cap);
 
 #ifdef __cplusplus
 }

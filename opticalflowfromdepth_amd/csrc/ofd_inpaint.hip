@@ -40,12 +40,33 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <algorithm>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <tuple>
+#include <vector>
+
 #include "ofd_fw.h"
 #include "ofd_inpaint.h"
 
 #pragma clang fp contract(off)
 
 namespace {
+
+// Diagnostic build only (tools/probe_ip.hip defines OFD_IP_STAMPS): thread 0
+// of the first block of each path of a hole-layer launch records shader-clock
+// stamps along the per-hole chain; the product build compiles them out.
+#ifdef OFD_IP_STAMPS
+__device__ unsigned long long *g_ip_stamps;
+__device__ __forceinline__ void ip_stamp(unsigned slot, unsigned k) {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    if (g_ip_stamps) g_ip_stamps[slot * 8 + k] = __builtin_amdgcn_s_memtime();
+}
+#define IP_STAMP(slot, k, cond) do { if (cond) ip_stamp(slot, k); } while (0)
+#else
+#define IP_STAMP(slot, k, cond) do { } while (0)
+#endif
 
 constexpr float T_FAR = 1.0e6f;
 // per-pixel code: bit 15 hole, bit 14 outer ring, bit 13 far known, low 13
@@ -554,6 +575,7 @@ __device__ __forceinline__ void telea_pixel_r3(const Img &m, int y, int x, unsig
 #pragma unroll
         for (int b = -3; b <= 3; ++b)
             if (in_disk3(a, b) && (a || b)) tk[pidx(a, b)] = (IN(a, b) || !inimg(a, b)) ? T_FAR : tk[pidx(a, b)];
+    IP_STAMP(2 * L, 2, threadIdx.x == 0 && blockIdx.x == 0);
     // fm_dist<false>
     const float tij = min4f(fm_solve(tk[pidx(-1, 0)], IN(-1, 0), tk[pidx(0, -1)], IN(0, -1)),
                             fm_solve(tk[pidx(1, 0)], IN(1, 0), tk[pidx(0, -1)], IN(0, -1)),
@@ -648,11 +670,14 @@ __device__ __forceinline__ void telea_pixel_r3(const Img &m, int y, int x, unsig
             }
         const float sat =
             float(double(Ia / s) + double(Jx + Jy) / (sqrt(double(Jx * Jx + Jy * Jy)) + double(1.0e-20f)) + double(0.5f));
+        IP_STAMP(2 * L, 3, threadIdx.x == 0 && blockIdx.x == 0);
         m.out[int64_t(c) * m.HW + p] = float(sat_u8(sat));
     }
 }
 
 // ---------------------------------------------------------------- SORT
+// After SCATTER, cursor[k] holds the END of bin k (its start + hist[k]); the
+// layer launches read both.
 // Counting sort of the chunk's ring pixels and holes by layer, chip-wide:
 // bins 0 .. nring-1 = ring layers 1 .., bins nring .. = hole layers 1 ..; an
 // entry is bl * HW + p (chunk-local image bl, pixel p).  HIST and SCATTER
@@ -695,15 +720,22 @@ __global__ __launch_bounds__(kSortThreads) void ip_hist_kernel(const uint16_t *_
         if (h[k]) atomicAdd(&hist[k], h[k]);
 }
 
-// cursor[k] = exclusive prefix sum of hist (one workgroup)
+// cursor[k] = exclusive prefix sum of hist (one workgroup); meta[0] = the
+// deepest non-empty hole layer (0: no holes), which bounds the device-side
+// layer loop of the deep tail kernel.
 __global__ __launch_bounds__(1024) void ip_scan_kernel(const unsigned *__restrict__ hist, unsigned *__restrict__ cursor,
-                                                       int n) {
+                                                       int n, int nring, unsigned *__restrict__ meta) {
     __shared__ unsigned wsum[16];
+    __shared__ unsigned lmax;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int per = (n + 1023) / 1024;
     const int beg = min(tid * per, n), end = min(beg + per, n);
-    unsigned sum = 0;
-    for (int i = beg; i < end; ++i) sum += hist[i];
+    if (tid == 0) lmax = 0;
+    unsigned sum = 0, lm = 0;
+    for (int i = beg; i < end; ++i) {
+        sum += hist[i];
+        if (i >= nring && hist[i]) lm = unsigned((i - nring) / 2 + 1);
+    }
     unsigned incl = sum;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -712,6 +744,7 @@ __global__ __launch_bounds__(1024) void ip_scan_kernel(const unsigned *__restric
     }
     if (lane == 63) wsum[wave] = incl;
     __syncthreads();
+    if (lm) atomicMax(&lmax, lm);
     if (tid == 0) {
         unsigned acc = 0;
         for (int k = 0; k < 16; ++k) {
@@ -725,6 +758,10 @@ __global__ __launch_bounds__(1024) void ip_scan_kernel(const unsigned *__restric
     for (int i = beg; i < end; ++i) {
         cursor[i] = excl;
         excl += hist[i];
+    }
+    if (tid == 0) {
+        meta[0] = lmax;
+        meta[1] = 0u;  // the deep tail kernel's barrier counter
     }
 }
 
@@ -753,6 +790,7 @@ __global__ __launch_bounds__(kSortThreads) void ip_scatter_kernel(const uint16_t
 
 // ---------------------------------------------------------------- LAYERS
 // One launch per layer over every image of the chunk, one thread per pixel.
+__device__ __forceinline__ unsigned blocks_for_dev(unsigned n, unsigned per) { return (n + per - 1u) / per; }
 struct Chunk {
     const uint16_t *code;
     float *T;
@@ -781,22 +819,30 @@ __device__ __forceinline__ Img image_of(const Chunk &ch, uint32_t e, int &y, int
     return m;
 }
 
-// outer band (icvCalcFMM over the ring): ring layer L
-__global__ __launch_bounds__(256) void ip_ring_layer_kernel(Chunk ch, const uint32_t *__restrict__ list, unsigned n,
-                                                            unsigned L) {
-    const unsigned i = blockIdx.x * 256u + threadIdx.x;
-    if (i >= n) return;
-    int y, x;
-    int64_t p;
-    const Img m = image_of(ch, list[i], y, x, p);
-    m.T[p] = fm_dist<true>(m, y, x, L);
+// Layer launches read their sizes and list offsets from the device (the
+// sort's hist / cursor), so the host never waits for them: a fixed grid walks
+// each list grid-stride.
+
+// outer band (icvCalcFMM over the ring): ring layer L = bin L - 1
+__global__ __launch_bounds__(256) void ip_ring_layer_kernel(Chunk ch, const uint32_t *__restrict__ list,
+                                                            const unsigned *__restrict__ hist,
+                                                            const unsigned *__restrict__ cursor, unsigned L) {
+    const unsigned n = hist[L - 1];
+    const uint32_t *lst = list + (cursor[L - 1] - n);  // SCATTER advanced cursor[] to each bin's end
+    for (unsigned i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
+        int y, x;
+        int64_t p;
+        const Img m = image_of(ch, lst[i], y, x, p);
+        m.T[p] = fm_dist<true>(m, y, x, L);
+    }
 }
 
-// the outer band's distances are negative (icvCalcFMM negate = true)
+// the outer band's distances are negative (icvCalcFMM negate = true): every
+// ring entry, bins 0 .. nring - 1 (list[0, end of bin nring - 1))
 __global__ __launch_bounds__(256) void ip_negate_kernel(float *__restrict__ T, const uint32_t *__restrict__ list,
-                                                        unsigned n) {
-    const unsigned i = blockIdx.x * 256u + threadIdx.x;
-    if (i < n) T[list[i]] = -T[list[i]];
+                                                        const unsigned *__restrict__ cursor, int nring) {
+    const unsigned n = cursor[nring - 1];
+    for (unsigned i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) T[list[i]] = -T[list[i]];
 }
 
 // hole layer L: distance, then every channel's Telea colour
@@ -814,11 +860,13 @@ __device__ __forceinline__ void hole_patch(const Chunk &ch, const uint32_t *__re
     int y, x;
     int64_t p;
     const Img m = image_of(ch, list[h], y, x, p);
+    IP_STAMP(2 * L, 1, i == 0);
     if (kCS == 1) {
         telea_pixel_r3<false>(m, y, x, L, p, 0, m.C);  // the sort put only radius-3 interior holes here
     } else {
         for (int c = int(c0); c < m.C; c += kCS) telea_pixel_r3<false>(m, y, x, L, p, c, c + 1);  // C >= 1
     }
+    IP_STAMP(2 * L, 4, i == 0);
 }
 
 __device__ __forceinline__ float rl(float v, int j) {
@@ -922,7 +970,27 @@ struct WavePatch {
     int fl[kPatchN];                // bit 0: inside the image, bit 1: INSIDE (hole of layer >= L)
     float t[kPatchN];               // T (raw)
     int sv[kChanGroup][kPatchN];    // sample() of the current channel group
+    float4 q[64][kChanGroup];       // per window position, per channel: (w*sc, w*gix*rx, w*giy*ry, w)
 };
+
+// cv2's distance weight dst = 1 / (|r|^2 * sqrt(|r|^2)) (double, rounded to
+// float) for the integer |r|^2 of a radius-3 window: the values the
+// double expression gives, bit for bit (host IEEE double = device double).
+__device__ __forceinline__ float dst_r3(int len2) {
+    switch (len2) {
+        case 1: return 0x1p+0f;
+        case 2: return 0x1.6a09e6p-2f;
+        case 4: return 0x1p-3f;
+        case 5: return 0x1.6e5b7ep-4f;
+        case 8: return 0x1.6a09e6p-5f;
+        default: return 0x1.2f684cp-5f;  // 9
+    }
+}
+
+// The 28 positions of the radius-3 disk (centre excluded) in raster order of
+// the 7 x 7 window, as window indices (dy + 3) * 7 + (dx + 3).
+__device__ constexpr int kDisk3[28] = {3,  8,  9,  10, 11, 12, 15, 16, 17, 18, 19, 21, 22, 23,
+                                       25, 26, 27, 29, 30, 31, 32, 33, 36, 37, 38, 39, 40, 45};
 
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -937,6 +1005,7 @@ __device__ __forceinline__ void hole_wave_lds(const Chunk &ch, const uint32_t *_
     int y, x;
     int64_t p;
     const Img m = image_of(ch, list[i], y, x, p);
+    IP_STAMP(2 * L + 1, 1, i == 0 && lane == 0);
     const int H = m.H, W = m.W, R = range, D = 2 * range + 1, npos = D * D;
     int64_t qe[2];
     unsigned hge[2];  // sample()'s test: hole of layer >= L
@@ -966,6 +1035,7 @@ __device__ __forceinline__ void hole_wave_lds(const Chunk &ch, const uint32_t *_
         }
     }
     wave_lds_sync();
+    IP_STAMP(2 * L + 1, 2, i == 0 && lane == 0);
     auto IN = [&](int e) -> bool { return (P.fl[e] & 2) != 0; };
     auto TV = [&](int e, bool &in) -> float {
         const int f = P.fl[e];
@@ -1008,10 +1078,6 @@ __device__ __forceinline__ void hole_wave_lds(const Chunk &ch, const uint32_t *_
             }
         }
         wave_lds_sync();
-        float Ia[kChanGroup], Jx[kChanGroup], Jy[kChanGroup];
-#pragma unroll
-        for (int c = 0; c < kChanGroup; ++c) Ia[c] = Jx[c] = Jy[c] = 0.f;
-        float s = 1.0e-20f;
         // npos <= 49: one pass
         const int idx = lane;
         const int k = y - R + idx / D, l = x - R + idx % D;
@@ -1025,11 +1091,11 @@ __device__ __forceinline__ void hole_wave_lds(const Chunk &ch, const uint32_t *_
             const int km = pk + (k == 0), kp = pk - (k == H - 1), lm = pl + (l == 0), lp = pl - (l == W - 1);
             const float ry = float(y - k), rx = float(x - l);
             const float len2 = rx * rx + ry * ry;
-            const float dst = float(1. / (double(len2) * sqrt(double(len2))));
+            const float dst = R <= 3 ? dst_r3(int(len2)) : float(1. / (double(len2) * sqrt(double(len2))));
             const float lev = float(1. / (1 + fabs(double(P.t[e] - tij))));
             float dir = rx * gtx + ry * gty;
-            if (fabs(double(dir)) <= 0.01) dir = 0.000001f;
-            w = float(fabs(double(dst * lev * dir)));
+            if (fabsf(dir) <= 0.01f) dir = 0.000001f;  // |dir| <= 0.01 (double) <=> |dir| <= 0.01f: no float lies between
+            w = fabsf(dst * lev * dir);                // float(fabs(double(f))) == fabsf(f)
             const bool nr = !IN(e + 1), nl = !IN(e - 1), nd = !IN(e + kPatch), nu = !IN(e - kPatch);
             auto S = [&](int c, int a, int b) -> int { return P.sv[c][a * kPatch + b]; };
             for (int c = 0; c < nc; ++c) {
@@ -1047,49 +1113,272 @@ __device__ __forceinline__ void hole_wave_lds(const Chunk &ch, const uint32_t *_
                 ty[c] = w * (giy * ry);
             }
         }
+        // The sums run over the window in raster order (cv2's k, l loops).
+        // Transposed through LDS: lane idx leaves its position's terms, then
+        // lane c < nc walks the positions in order and accumulates channel c
+        // (and s, the same sequence in every channel lane) -- four independent
+        // chains per lane instead of a wave-wide fold of 4 x nc + 1 readlanes
+        // per position.
         const uint64_t vm = __ballot(valid);
-        for (int j = 0; j < 64; ++j) {
-            if (!((vm >> j) & 1ull)) continue;  // uniform
-            for (int c = 0; c < nc; ++c) {
-                Ia[c] += rl(ti[c], j);
-                Jx[c] -= rl(tx[c], j);
-                Jy[c] -= rl(ty[c], j);
+#pragma unroll
+        for (int c = 0; c < kChanGroup; ++c)
+            if (c < nc) P.q[lane][c] = make_float4(ti[c], tx[c], ty[c], w);
+        wave_lds_sync();
+        if (lane < nc) {
+            float a = 0.f, jx = 0.f, jy = 0.f, sw = 1.0e-20f;
+            if (R == 3) {
+                // the disk's 28 positions, unconditionally: a position that is
+                // not used carries +0 terms, and adding / subtracting +0 leaves
+                // every running sum unchanged (a and sw never hold -0: their
+                // terms are >= 0), so the sums equal cv2's skipping ones
+#pragma unroll
+                for (int b0 = 0; b0 < 28; b0 += 7) {
+                    float4 v[7];
+#pragma unroll
+                    for (int t = 0; t < 7; ++t) v[t] = P.q[kDisk3[b0 + t]][lane];
+#pragma unroll
+                    for (int t = 0; t < 7; ++t) {
+                        a += v[t].x;
+                        jx -= v[t].y;
+                        jy -= v[t].z;
+                        sw += v[t].w;
+                    }
+                }
+            } else {
+                for (int j = 0; j < npos; ++j) {
+                    if (!((vm >> j) & 1ull)) continue;  // uniform
+                    const float4 v = P.q[j][lane];
+                    a += v.x;
+                    jx -= v.y;
+                    jy -= v.z;
+                    sw += v.w;
+                }
             }
-            s += rl(w, j);
-        }
-        if (lane == 0) {
-            for (int c = 0; c < nc; ++c) {
-                const float sat = float(double(Ia[c] / s) +
-                                        double(Jx[c] + Jy[c]) / (sqrt(double(Jx[c] * Jx[c] + Jy[c] * Jy[c])) + double(1.0e-20f)) +
-                                        double(0.5f));
-                m.out[(c0 + c) * m.HW + p] = float(sat_u8(sat));
-            }
+            IP_STAMP(2 * L + 1, 3, i == 0 && lane == 0 && c0 == 0);
+            const float sat = float(double(a / sw) + double(jx + jy) / (sqrt(double(jx * jx + jy * jy)) + double(1.0e-20f)) +
+                                    double(0.5f));
+            m.out[(c0 + lane) * m.HW + p] = float(sat_u8(sat));
         }
     }
     if (lane == 0) m.T[p] = tij;
+    IP_STAMP(2 * L + 1, 4, i == 0 && lane == 0);
 }
 
-// One launch per hole layer: blocks [0, nbp) take the patch-interior holes
-// (thread per hole), the rest the others (wave per hole).  The two sets of a
-// layer are independent, so they share the launch; every block runs one path.
-template <int kCS>
-__global__ __launch_bounds__(256) void ip_hole_layer_kernel(Chunk ch, const uint32_t *__restrict__ lp, unsigned np,
-                                                            unsigned nbp, const uint32_t *__restrict__ lw, unsigned nw,
-                                                            unsigned L, int range) {
+// One hole layer over the grid.  The layer's two bins (patch-interior holes,
+// the others) are read from the device.  A thin layer (at most thin_cap
+// holes, radius <= 3) runs every hole on the wave path, whose per-hole chain
+// is the shorter one; otherwise blocks [0, gb) take the patch-interior holes
+// (thread per hole, or kCS threads per hole up to kCsSplitMax holes) and the
+// rest of the grid the others (wave per hole), each part grid-stride.  The
+// two sets of a layer are independent; every block runs one path.
+__device__ __forceinline__ void hole_layer_body(const Chunk &ch, const uint32_t *__restrict__ list,
+                                                const unsigned *__restrict__ hist, const unsigned *__restrict__ cursor,
+                                                int nring, unsigned L, int range, unsigned thin_cap, WavePatch *patch) {
+    const int bi = nring + 2 * (int(L) - 1);
+    const unsigned ni = hist[bi], nw = hist[bi + 1];
+    if (ni + nw == 0u) return;
+    // SCATTER advanced cursor[] to each bin's end: a bin starts at cursor - count
+    const uint32_t *lp = list + (cursor[bi] - ni), *lw = list + (cursor[bi + 1] - nw);
+    const unsigned wave = threadIdx.x >> 6, G = gridDim.x;
+    IP_STAMP(2 * L, 0, blockIdx.x == 0 && threadIdx.x == 0);
+    IP_STAMP(2 * L + 1, 0, blockIdx.x == G - 1 && threadIdx.x == 0);
+    if (range <= 3 && ni + nw <= thin_cap) {
+        for (unsigned h = blockIdx.x * 4u + wave; h < ni + nw; h += G * 4u) {
+            if (h < ni)
+                hole_wave_lds(ch, lp, ni, h, L, range, patch[wave]);
+            else
+                hole_wave_lds(ch, lw, nw, h - ni, L, range, patch[wave]);
+        }
+        return;
+    }
+    const unsigned cs = ni > kCsSplitMax ? 1u : 3u;
+    const unsigned bt = blocks_for_dev(ni * cs, 256u), bw = blocks_for_dev(nw, 4u);
+    // split the grid in proportion to the two parts' blocks (each part at least one block)
+    unsigned gb = bt + bw <= G ? bt : (bw == 0u ? G : (bt == 0u ? 0u : max(1u, unsigned(uint64_t(G) * bt / (bt + bw)))));
+    if (bw && gb >= G) gb = G - 1u;
+    if (blockIdx.x < gb) {
+        for (unsigned i = blockIdx.x * 256u + threadIdx.x; i < ni * cs; i += gb * 256u) {
+            if (cs == 1u)
+                hole_patch<1>(ch, lp, ni, i, L);
+            else
+                hole_patch<3>(ch, lp, ni, i, L);
+        }
+    } else {
+        const unsigned gw = G - gb;
+        for (unsigned h = (blockIdx.x - gb) * 4u + wave; h < nw; h += gw * 4u) {
+            if (range <= 3)
+                hole_wave_lds(ch, lw, nw, h, L, range, patch[wave]);
+            else
+                hole_wave(ch, lw, nw, h, L, range);
+        }
+    }
+}
+
+// One launch per hole layer L (the host launches layers 1 .. K).
+__global__ __launch_bounds__(256) void ip_hole_layer_kernel(Chunk ch, const uint32_t *__restrict__ list,
+                                                            const unsigned *__restrict__ hist,
+                                                            const unsigned *__restrict__ cursor, int nring, unsigned L,
+                                                            int range, unsigned thin_cap) {
     __shared__ WavePatch patch[4];
-    if (blockIdx.x < nbp)
-        hole_patch<kCS>(ch, lp, np, blockIdx.x * 256u + threadIdx.x, L);
-    else if (range <= 3)
-        hole_wave_lds(ch, lw, nw, (blockIdx.x - nbp) * 4u + (threadIdx.x >> 6), L, range, patch[threadIdx.x >> 6]);
-    else
-        hole_wave(ch, lw, nw, (blockIdx.x - nbp) * 4u + (threadIdx.x >> 6), L, range);
+    hole_layer_body(ch, list, hist, cursor, nring, L, range, thin_cap, patch);
+}
+
+// Grid barrier of the deep tail kernel (every workgroup resident): a
+// monotonic arrival counter, lane 0 of each workgroup releasing its stores at
+// agent scope before arriving and acquiring after the last arrival
+// (MI355X_MICROARCH.md, inter-workgroup visibility).
+__device__ __forceinline__ void tail_grid_sync(unsigned *count, unsigned nblocks, unsigned &gen) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned target = (++gen) * nblocks;
+        __hip_atomic_fetch_add(count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // bounded: a workgroup that never arrives (it cannot happen with one
+        // resident workgroup per CU) ends the wait instead of hanging the GPU
+        for (unsigned spin = 0; spin < (1u << 26) &&
+                                __hip_atomic_load(count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target;
+             ++spin)
+            __builtin_amdgcn_s_sleep(2);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+}
+
+// The layers beyond the ones the host launched (L0 .. meta[0], the deepest
+// layer the sort found): one persistent launch, a grid barrier between
+// layers.  Exits at once when meta[0] < L0 (the usual case: the host sizes
+// its launches from the previous call's depth).
+__global__ __launch_bounds__(256) void ip_hole_tail_kernel(Chunk ch, const uint32_t *__restrict__ list,
+                                                           const unsigned *__restrict__ hist,
+                                                           const unsigned *__restrict__ cursor, unsigned *meta,
+                                                           int nring, unsigned L0, int range, unsigned thin_cap) {
+    __shared__ WavePatch patch[4];
+    const unsigned lmax = meta[0];
+    unsigned gen = 0;
+    for (unsigned L = L0; L <= lmax; ++L) {
+        hole_layer_body(ch, list, hist, cursor, nring, L, range, thin_cap, patch);
+        if (L < lmax) tail_grid_sync(meta + 1, gridDim.x, gen);
+    }
 }
 
 inline unsigned blocks_for(unsigned n, unsigned per) { return (n + per - 1) / per; }
 
+// Layers launched one by one before the deep tail kernel takes over, when no
+// earlier call at this shape has reported its depth yet.
+constexpr int kDefaultLayers = 64;
+
+// Layers of at most this many holes run every hole on the wave path
+// (OFD_IP_THIN or ofd_inpaint_set_schedule override; probes and tests).
+int g_thin_cap = -1, g_launch_layers = -1;
+unsigned thin_layer_cap() {
+    if (g_thin_cap >= 0) return unsigned(g_thin_cap);
+    static const unsigned v = [] {
+        const char *e = getenv("OFD_IP_THIN");
+        return e ? unsigned(atoi(e)) : 4096u;
+    }();
+    return v;
+}
+
+// Grid of a layer launch when its size is unknown, and the cap otherwise:
+// 8 workgroups per CU.
+unsigned default_layer_grid() {
+    static const unsigned v = [] {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                    hipSuccess || cus <= 0)
+            cus = 256;
+        return unsigned(cus) * 8u;
+    }();
+    return v;
+}
+
+// The deep tail kernel's grid barrier needs every workgroup resident: one
+// 256-thread workgroup per CU (its registers and LDS admit two).
+unsigned tail_grid() {
+    static const unsigned v = [] {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                    hipSuccess || cus <= 0)
+            cus = 256;
+        return unsigned(cus);
+    }();
+    return v;
+}
+
+// Per-shape layer statistics of the previous call, read back without ever
+// blocking the host: every call enqueues an asynchronous copy of its layer
+// histogram and depth into pinned memory behind an event; a later call uses
+// them (to size its grids and the number of layer launches) only once that
+// event has completed.  They steer launch sizes only, never results.
+struct LaggedStats {
+    std::mutex mu;
+    unsigned *pinned = nullptr;  // [kMaxBins + 1]: hist, then the depth (meta[0])
+    hipEvent_t ev = nullptr;
+    bool pending = false;
+    std::vector<unsigned> hist;  // last completed copy
+    unsigned lmax = 0, ring = 0;
+    bool valid = false;
+    struct View {
+        bool valid = false;
+        std::vector<unsigned> hist;
+        unsigned lmax = 0, ring = 0;
+    };
+    View snapshot(int nbins, int nring) {
+        std::lock_guard<std::mutex> lk(mu);
+        if (pending && hipEventQuery(ev) == hipSuccess) {
+            hist.assign(pinned, pinned + nbins);
+            lmax = pinned[kMaxBins];
+            ring = 0;
+            for (int k = 0; k < nring && k < nbins; ++k) ring += hist[size_t(k)];
+            valid = true;
+            pending = false;
+        }
+        View v;
+        v.valid = valid && int(hist.size()) == nbins;
+        if (v.valid) {
+            v.hist = hist;
+            v.lmax = lmax;
+            v.ring = ring;
+        }
+        return v;
+    }
+    void record(const unsigned *dhist, const unsigned *dmeta, int nbins, hipStream_t st) {
+        std::lock_guard<std::mutex> lk(mu);
+        if (pending) return;  // the previous copy is still in flight: keep it
+        if (!pinned) {
+            if (hipHostMalloc(reinterpret_cast<void **>(&pinned), (kMaxBins + 1) * sizeof(unsigned),
+                              hipHostMallocDefault) != hipSuccess) {
+                pinned = nullptr;
+                return;
+            }
+            if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return;
+        }
+        if (hipMemcpyAsync(pinned, dhist, size_t(nbins) * 4, hipMemcpyDeviceToHost, st) != hipSuccess) return;
+        if (hipMemcpyAsync(pinned + kMaxBins, dmeta, 4, hipMemcpyDeviceToHost, st) != hipSuccess) return;
+        if (hipEventRecord(ev, st) == hipSuccess) pending = true;
+    }
+};
+
+LaggedStats &lagged_stats(int64_t nb, int64_t H, int64_t W, int r) {
+    static std::mutex mu;
+    static std::map<std::tuple<int64_t, int64_t, int64_t, int>, std::unique_ptr<LaggedStats>> m;
+    std::lock_guard<std::mutex> lk(mu);
+    auto &p = m[std::make_tuple(nb, H, W, r)];
+    if (!p) p.reset(new LaggedStats());
+    return *p;
+}
+
 }  // namespace
 
 extern "C" {
+
+int ofd_inpaint_set_schedule(int launch_layers, int thin_cap) {
+    g_launch_layers = launch_layers < 0 ? -1 : launch_layers;
+    g_thin_cap = thin_cap < 0 ? -1 : thin_cap;
+    return OFD_FW_OK;
+}
 
 size_t ofd_inpaint_workspace_bytes(int64_t B, int64_t H, int64_t W) {
     if (B <= 0 || H <= 0 || W <= 0) return 0;
@@ -1108,7 +1397,7 @@ int ofd_inpaint_telea_f32(const float *img, const float *valid, const float *col
     const int nring = 2 * r;  // ring layers 1 .. 2r-1 (a Chebyshev-r neighbour is <= 2r away in L1)
     const int64_t HW = H * W;
     const size_t pi = per_image(H, W);
-    const size_t fixed = 2 * align256(size_t(kMaxBins) * 4);
+    const size_t fixed = 2 * align256(size_t(kMaxBins) * 4) + 256;
     if (!workspace || (reinterpret_cast<uintptr_t>(workspace) & 255u)) return OFD_FW_EWORKSPACE;
     if (workspace_bytes < fixed + pi) return OFD_FW_EWORKSPACE;
     int64_t G = int64_t((workspace_bytes - fixed) / pi);
@@ -1116,11 +1405,14 @@ int ofd_inpaint_telea_f32(const float *img, const float *valid, const float *col
     if (G > gcap) G = gcap;
     if (G > B) G = B;
     hipStream_t st = static_cast<hipStream_t>(stream);
-    unsigned *hist = reinterpret_cast<unsigned *>(workspace);
-    unsigned *cursor = reinterpret_cast<unsigned *>(static_cast<char *>(workspace) + align256(size_t(kMaxBins) * 4));
-    const IpWs w = carve(static_cast<char *>(workspace) + fixed, G, HW);
+    char *wsb = static_cast<char *>(workspace);
+    unsigned *hist = reinterpret_cast<unsigned *>(wsb);
+    unsigned *cursor = reinterpret_cast<unsigned *>(wsb + align256(size_t(kMaxBins) * 4));
+    unsigned *meta = reinterpret_cast<unsigned *>(wsb + 2 * align256(size_t(kMaxBins) * 4));
+    const IpWs w = carve(wsb + fixed, G, HW);
     const int nbins = nring + 2 * int(H + W);
-    unsigned hh[kMaxBins];
+    const unsigned thin_cap = thin_layer_cap();
+    const unsigned gdef = default_layer_grid();
     for (int64_t b0 = 0; b0 < B; b0 += G) {
         const int64_t nb = B - b0 < G ? B - b0 : G;
         const int64_t total = nb * HW;
@@ -1146,47 +1438,45 @@ int ofd_inpaint_telea_f32(const float *img, const float *valid, const float *col
         const unsigned sblocks = unsigned((total + kSortSpan - 1) / kSortSpan);
         hipLaunchKernelGGL(ip_hist_kernel, dim3(sblocks), dim3(kSortThreads), 0, st, w.code, hist, total, nring,
                            int(H), int(W), r == 3);
-        hipLaunchKernelGGL(ip_scan_kernel, dim3(1), dim3(1024), 0, st, hist, cursor, nbins);
-        // the layer counts size the per-layer launches: one host round trip per chunk
-        e = hipMemcpyAsync(hh, hist, size_t(nbins) * 4, hipMemcpyDeviceToHost, st);
-        if (e == hipSuccess) e = hipStreamSynchronize(st);
-        if (e != hipSuccess) return int(e);
+        hipLaunchKernelGGL(ip_scan_kernel, dim3(1), dim3(1024), 0, st, hist, cursor, nbins, nring, meta);
         hipLaunchKernelGGL(ip_scatter_kernel, dim3(sblocks), dim3(kSortThreads), 0, st, w.code, cursor, w.list, total,
                            nring, int(H), int(W), r == 3);
+        // Launch sizes: the layer counts stay on the device (each launch reads
+        // its own); the host only picks grid sizes and how many layers to
+        // launch, from the previous call's counts at this shape when those have
+        // arrived (LaggedStats) -- the deep tail kernel covers whatever layers
+        // lie beyond, so the result never depends on them.
+        LaggedStats::View lag = lagged_stats(nb, H, W, r).snapshot(nbins, nring);
+        auto grid_for_bin = [&](int bin, unsigned per_block, unsigned per_item) -> unsigned {
+            if (!lag.valid) return gdef;
+            const uint64_t n = uint64_t(lag.hist[size_t(bin)]) * per_item;
+            const uint64_t g = (n + per_block - 1) / per_block;
+            return unsigned(g < 16 ? 16 : (g > gdef ? gdef : g + g / 8 + 4));
+        };
         const Chunk ch{w.code, w.T, img, out, int(C), int(H), int(W), HW, b0};
-        unsigned off = 0;
-        for (int L = 1; L < nring; ++L) {  // outer band, then negated
-            const unsigned n = hh[L - 1];
-            if (n)
-                hipLaunchKernelGGL(ip_ring_layer_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, st, ch, w.list + off,
-                                   n, unsigned(L));
-            off += n;
-        }
-        off += hh[nring - 1];  // always empty (ring layers stop at 2r - 1)
-        if (off)
-            hipLaunchKernelGGL(ip_negate_kernel, dim3(blocks_for(off, 256)), dim3(256), 0, st, w.T, w.list, off);
-        for (int L = 1; nring + 2 * (L - 1) < nbins; ++L) {  // holes: patch-interior, then the others
-            const unsigned ni = hh[nring + 2 * (L - 1)], nw = hh[nring + 2 * (L - 1) + 1];
-            static const bool dbg = getenv("OFD_IP_DEBUG") != nullptr;  // per-layer sizes (tools/ip_layers.py)
-            if (dbg && ni + nw) fprintf(stderr, "ip layer %d interior %u other %u\n", L, ni, nw);
-            static const int cs = [] {  // probe knob OFD_IP_CS: threads per interior hole (1 or 3)
-                const char *e = getenv("OFD_IP_CS");
-                return e && atoi(e) == 1 ? 1 : 3;
-            }();
-            // a big layer is throughput-bound: one thread per hole (the channel split
-            // recomputes the weights per channel); small layers are latency-bound
-            const int csl = ni > kCsSplitMax ? 1 : cs;
-            const unsigned nbp = blocks_for(ni * unsigned(csl), 256), nbw = blocks_for(nw, 4);
-            if (nbp + nbw) {
-                if (csl == 1)
-                    hipLaunchKernelGGL(ip_hole_layer_kernel<1>, dim3(nbp + nbw), dim3(256), 0, st, ch, w.list + off, ni,
-                                       nbp, w.list + off + ni, nw, unsigned(L), r);
-                else
-                    hipLaunchKernelGGL(ip_hole_layer_kernel<3>, dim3(nbp + nbw), dim3(256), 0, st, ch, w.list + off, ni,
-                                       nbp, w.list + off + ni, nw, unsigned(L), r);
+        for (int L = 1; L < nring; ++L)  // outer band, then negated
+            hipLaunchKernelGGL(ip_ring_layer_kernel, dim3(grid_for_bin(L - 1, 256, 1)), dim3(256), 0, st, ch, w.list,
+                               hist, cursor, unsigned(L));
+        hipLaunchKernelGGL(ip_negate_kernel, dim3(lag.valid ? std::max(16u, std::min(gdef, lag.ring / 256u + 4u)) : gdef),
+                           dim3(256), 0, st, w.T, w.list, cursor, nring);
+        const int lmax_launch = g_launch_layers >= 0 ? std::min(g_launch_layers, int(H + W))
+                                : int(lag.valid ? std::min<unsigned>(lag.lmax + 2u, unsigned(H + W)) : kDefaultLayers);
+        for (int L = 1; L <= lmax_launch; ++L) {
+            const int bi = nring + 2 * (L - 1);
+            unsigned g = gdef;
+            if (lag.valid) {
+                const unsigned ni = lag.hist[size_t(bi)], nwv = lag.hist[size_t(bi) + 1];
+                const unsigned cs = ni > kCsSplitMax ? 1u : 3u;
+                const unsigned need = (ni + nwv <= thin_cap) ? blocks_for(ni + nwv, 4)
+                                                              : blocks_for(ni * cs, 256) + blocks_for(nwv, 4);
+                g = std::max(16u, std::min(gdef, need + need / 8 + 4));
             }
-            off += ni + nw;
+            hipLaunchKernelGGL(ip_hole_layer_kernel, dim3(g), dim3(256), 0, st, ch, w.list, hist, cursor, nring,
+                               unsigned(L), r, thin_cap);
         }
+        hipLaunchKernelGGL(ip_hole_tail_kernel, dim3(tail_grid()), dim3(256), 0, st, ch, w.list, hist, cursor, meta,
+                           nring, unsigned(lmax_launch + 1), r, thin_cap);
+        lagged_stats(nb, H, W, r).record(hist, meta, nbins, st);
     }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? OFD_FW_OK : int(e);

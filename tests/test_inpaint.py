@@ -177,3 +177,52 @@ def test_inpaint_after_warp_headline_shape():
     got = ops.inpaint(rgb, valid, coll).cpu().numpy()
     exp = oracle.inpaint(rgb.cpu().numpy(), valid.cpu().numpy(), coll.cpu().numpy(), 3, layered=True)
     assert np.array_equal(got, exp)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sched", [(0, 0), (0, 1 << 30), (1, 0), (3, 64), (-1, -1)],
+                         ids=["tail-only-thread", "tail-only-wave", "1-launch", "3-launches-thin64", "default"])
+def test_inpaint_gpu_schedules_bit_exact(sched):
+    """Every schedule of the hole layers -- one launch per layer or the
+    persistent deep-tail kernel with grid barriers, thread or wave paths --
+    gives the layered oracle's bits (the schedule steers speed only)."""
+    from opticalflowfromdepth_amd import _native, forward_warp_flow, ops, synth
+    lib = _native.lib()
+    dev = torch.device("cuda:0")
+    cases = [c for c in _gpu_cases() if c[0] in ("bighole", "smooth96x128", "rand_r3_C3", "rand_r1_C4", "wide12x1100")]
+    obj, flow, depth = synth.stage_one_batch([12345, 12377], 192, 256, dev)  # disparity + ego-motion holes
+    out, valid, coll = forward_warp_flow(obj, flow, depth)
+    cases.append(("warped", (out[:, 0:3] * valid).cpu().numpy(), valid.cpu().numpy(), coll.cpu().numpy(), 3))
+    lib.ofd_inpaint_set_schedule(*sched)
+    try:
+        for name, img, v, c, r in cases:
+            exp = oracle.inpaint(img, v, c, r, layered=True)
+            for rep in range(2):  # the second call sees the first one's layer statistics
+                got = ops.inpaint(torch.from_numpy(img).to(dev), torch.from_numpy(v).to(dev),
+                                  torch.from_numpy(c).to(dev), radius=r)
+                torch.cuda.synchronize()
+                bad = np.argwhere(got.cpu().numpy() != exp)
+                assert bad.size == 0, f"{name} {sched} rep{rep}: {len(bad)} differing, first {bad[:5].tolist()}"
+    finally:
+        lib.ofd_inpaint_set_schedule(-1, -1)
+
+
+def test_layered_vs_sequential_divergence_on_warped_images():
+    """The documented divergence of the layered fill from the
+    sequential (cv2-order) restatement on the real workload's kind of image:
+    warped 384x512 RGB with disparity holes and ego-motion border strips,
+    measured over the filled values.  The bound asserted here is the spec;
+    bench.py reports the same statistics on the 768x1024 batch."""
+    from opticalflowfromdepth_amd import synth
+    seeds = [12345, 12346, 12377, 12378]          # 2 disparity + 2 ego-motion
+    obj, flow, depth = synth.stage_one_batch(seeds, 384, 512, "cpu")
+    o, v, c = oracle.fw_flow(obj.numpy(), flow.numpy(), depth.numpy())
+    rgb = o[:, 0:3] * v
+    seq = oracle.inpaint(rgb, v, c, 3, layered=False)
+    lay = oracle.inpaint(rgb, v, c, 3, layered=True)
+    hole = np.broadcast_to(oracle.inpaint_mask(v, c)[:, None] != 0, seq.shape)
+    d = np.abs(seq.astype(np.int32) - lay.astype(np.int32))[hole]
+    assert d.size > 0
+    stats = dict(mean=float(d.mean()), p99=float(np.percentile(d, 99)), frac_over_8=float((d > 8).mean()),
+                 frac_over_32=float((d > 32).mean()))
+    assert stats["mean"] < 8.0 and stats["p99"] < 64 and stats["frac_over_32"] < 0.05, stats
