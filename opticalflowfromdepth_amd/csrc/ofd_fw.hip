@@ -75,7 +75,8 @@ constexpr int SBW = 16, SBH = 4;          // source block = one wave (64 px)
 constexpr int SEGB = 8;                   // source blocks per segment (128 x 4 px)
 constexpr int MAX_TILES_PER_BLOCK = 12;   // wider boxes go through the global path
 constexpr int kSplatU = 2;                // 4-block slots in flight per wave (SPLAT, f32 coords; 3 spills)
-constexpr int kBinSPW = 1;                // segments per BIN wave (bin_kernel)
+constexpr int kBinSPW = 1;                // segments per BIN wave (bin_kernel; 2 measured slower, also for depth-only sources)
+
 
 // Default chunk: 64M source pixels (85 images of 768x1024, a ~830 MB slab).
 // Every kernel of a chunk then has a grid many times the resident slots
@@ -782,18 +783,9 @@ struct SplatCfg {
                          kMap = kMap_;
 };
 
-// One target tile (linear index `lin` of the chunk's band-major tile order).
-// Every barrier is LDS-only: global loads are consumed by the thread that
-// issued them, and the published stores are never waited for.
-template <typename Coords, bool kVec, bool kFuse, bool kStamp, typename Cfg, typename E = float>
-__device__ __forceinline__ void splat_tile(TileLds &L, unsigned lin, const Coords &co, const float *__restrict__ depth,
-                                           const SplatIO &io, const ChunkArgs &a, int H, int W, int64_t HW,
-                                           const TileGeom &g, unsigned long long *stamps) {
-    unsigned long long *ph = kStamp ? stamps + 8 * lin : nullptr;
-    if constexpr (kStamp) { if (threadIdx.x == 0) ph[0] = wall_clock64(); }
-
-    const Ws &ws = a.ws;
-    int bl, tile;
+// (image, tile) of linear index `lin` of the chunk's tile order
+template <typename Cfg>
+__device__ __forceinline__ void tile_of(unsigned lin, const ChunkArgs &a, const TileGeom &g, int &bl, int &tile) {
     if constexpr (Cfg::kMap == 0) {
         band_major_tile(lin, a.nimg, g, bl, tile);
     } else if constexpr (Cfg::kMap == 1) {  // whole images, image k, k+8, ... on XCD k
@@ -808,6 +800,66 @@ __device__ __forceinline__ void splat_tile(TileLds &L, unsigned lin, const Coord
         bl = int(lin / unsigned(g.ntiles));
         tile = int(lin - unsigned(bl) * unsigned(g.ntiles));
     }
+}
+
+// The segments (SEGB source blocks) of image bl whose target-tile box holds
+// tile (txi, tyi), appended to L.seg; *cnt counts them (> kSegCap: too many,
+// the tile scans every block instead).  All loads of a thread in flight
+// together.
+template <typename Cfg>
+__device__ __forceinline__ void seg_scan(TileLds &L, unsigned *cnt, const ushort4 *segrec, const TileGeom &g, int txi,
+                                         int tyi) {
+    for (int s0 = threadIdx.x; s0 < g.nseg; s0 += Cfg::kThr * 4) {
+        ushort4 r[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int sidx = s0 + u * Cfg::kThr;
+            r[u] = sidx < g.nseg ? segrec[sidx] : empty_box();
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (box_has(r[u], txi, tyi)) {
+                const unsigned idx = atomicAdd(cnt, 1u);
+                if (idx < unsigned(kSegCap)) L.seg[idx] = unsigned(s0 + u * Cfg::kThr);
+            }
+        }
+    }
+}
+
+// Persistent SPLAT's tile queue (thread 0): the next tile, ~0u when every
+// queue is drained; the last workgroup to find them drained restores the
+// queue words for the next launch.
+__device__ __forceinline__ unsigned dequeue_tile(unsigned *queue, unsigned home, unsigned per, unsigned total,
+                                                 unsigned &drained) {
+    unsigned lin = ~0u;
+    for (unsigned k = 0; k < 8u && lin == ~0u; ++k) {
+        const unsigned qx = (home + k) & 7u;
+        if ((drained >> qx) & 1u) continue;
+        const unsigned idx = ~atomicSub(queue + qx, 1u);
+        const unsigned l = qx * per + idx;
+        if (idx < per && l < total) lin = l;
+        else drained |= 1u << qx;
+    }
+    if (lin == ~0u && ~atomicSub(queue + 8, 1u) == gridDim.x - 1u) {
+        // every other workgroup has finished dequeuing: restore the queues
+        for (int k = 0; k < 9; ++k) atomicExch(queue + k, ~0u);
+    }
+    return lin;
+}
+
+// One target tile (linear index `lin` of the chunk's band-major tile order).
+// Every barrier is LDS-only: global loads are consumed by the thread that
+// issued them, and the published stores are never waited for.
+template <typename Coords, bool kVec, bool kFuse, bool kStamp, typename Cfg, typename E = float>
+__device__ __forceinline__ void splat_tile(TileLds &L, unsigned lin, const Coords &co, const float *__restrict__ depth,
+                                           const SplatIO &io, const ChunkArgs &a, int H, int W, int64_t HW,
+                                           const TileGeom &g, unsigned long long *stamps) {
+    unsigned long long *ph = kStamp ? stamps + 8 * lin : nullptr;
+    if constexpr (kStamp) { if (threadIdx.x == 0) ph[0] = wall_clock64(); }
+
+    const Ws &ws = a.ws;
+    int bl, tile;
+    tile_of<Cfg>(lin, a, g, bl, tile);
     const unsigned fid = unsigned(bl) * unsigned(g.ntiles) + unsigned(tile);  // flag slot
     const int tyi = tile / g.tilesX, txi = tile - tyi * g.tilesX;
     const int x0 = txi * TW, y0 = tyi * TH;
@@ -825,22 +877,8 @@ __device__ __forceinline__ void splat_tile(TileLds &L, unsigned lin, const Coord
     for (int k = threadIdx.x; k < TW * TH; k += Cfg::kThr) L.zk[k] = KEY_UNTOUCHED;
     lds_barrier();
 
-    // ---- 1. segments whose box holds this tile (all loads of a thread in flight together)
-    for (int s0 = threadIdx.x; s0 < g.nseg; s0 += Cfg::kThr * 4) {
-        ushort4 r[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int sidx = s0 + u * Cfg::kThr;
-            r[u] = sidx < g.nseg ? segrec[sidx] : empty_box();
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            if (box_has(r[u], txi, tyi)) {
-                const unsigned idx = atomicAdd(&L.nseg, 1u);
-                if (idx < unsigned(kSegCap)) L.seg[idx] = unsigned(s0 + u * Cfg::kThr);
-            }
-        }
-    }
+    // ---- 1. segments whose box holds this tile
+    seg_scan<Cfg>(L, &L.nseg, segrec, g, txi, tyi);
     lds_barrier();
     if constexpr (kStamp) { if (threadIdx.x == 0) ph[4] = wall_clock64(); }
     const int nsel = int(L.nseg);
@@ -1087,7 +1125,11 @@ using SplitCfg = SplatCfg<512, 2, 8>;  // split engine: 4 workgroups / CU, light
 // thread (8 x C) in flight at once.  Measured at 64 x 768x1024, C = 6
 // (tools/probe_tile.py): 512 threads / 2 in flight / 4 per CU 702 us;
 // 512 / 8 / 2 per CU 675; as a persistent kernel 655; 256 threads 715.
-using FusedCfg = SplatCfg<512, 8, 4>;
+#ifndef OFD_PROBE_THR  // SPLAT workgroup shape: overridable only by the diagnostic probe build
+#define OFD_PROBE_THR 512
+#define OFD_PROBE_MINW 4
+#endif
+using FusedCfg = SplatCfg<OFD_PROBE_THR, 8, OFD_PROBE_MINW>;
 // coordinate sources that generate channels carry the generated values and a
 // division per source: 4 targets in flight keeps them inside 128 VGPRs
 // (Coords::kGenGT of them: 4 for the disparity source, 2 for the ego-motion
@@ -1130,22 +1172,7 @@ __global__ __launch_bounds__(Cfg::kThr, Cfg::kMinW) void splat_persist_kernel(Co
     const unsigned home = blockIdx.x % 8u;
     unsigned drained = 0;  // thread 0: queues seen empty
     for (;;) {
-        if (threadIdx.x == 0) {
-            unsigned lin = ~0u;
-            for (unsigned k = 0; k < 8u && lin == ~0u; ++k) {
-                const unsigned qx = (home + k) & 7u;
-                if ((drained >> qx) & 1u) continue;
-                const unsigned idx = ~atomicSub(queue + qx, 1u);
-                const unsigned l = qx * per + idx;
-                if (idx < per && l < total) lin = l;
-                else drained |= 1u << qx;
-            }
-            if (lin == ~0u && ~atomicSub(queue + 8, 1u) == gridDim.x - 1u) {
-                // every other workgroup has finished dequeuing: restore the queues
-                for (int k = 0; k < 9; ++k) atomicExch(queue + k, ~0u);
-            }
-            L.next = lin;
-        }
+        if (threadIdx.x == 0) L.next = dequeue_tile(queue, home, per, total, drained);
         lds_barrier();
         const unsigned lin = L.next;
         if (lin == ~0u) return;

@@ -227,7 +227,9 @@ def ego_motion_flow(depth: torch.Tensor, T: torch.Tensor) -> torch.Tensor:
     ys, xs = torch.meshgrid(torch.arange(h, device=dev), torch.arange(w, device=dev), indexing="ij")
     pix = torch.stack([xs.reshape(-1).float(), ys.reshape(-1).float(),
                        torch.ones(h * w, device=dev)], 0)                       # geometry.py:27-35
-    cam = torch.matmul(inv_K[:3, :3], pix).unsqueeze(0)                          # :38
+    # the reference's shapes exactly ([1,3,3] @ [1,3,HW]): a 2-D matmul takes
+    # another BLAS path on some hosts and rounds differently
+    cam = torch.matmul(inv_K[None, :3, :3], pix.unsqueeze(0))                    # :38
     cam = depth.reshape(B, 1, -1) * cam                                          # :39 (depth's dtype)
     cam = torch.cat([cam, torch.ones(B, 1, h * w, device=dev, dtype=cam.dtype)], 1).to(torch.float32)  # :40
     P = torch.matmul(K.unsqueeze(0), T.to(dev))[:, :3, :]                        # :57

@@ -45,9 +45,9 @@ extern "C" int probe_launch(int which, const float *obj, const float *flow, cons
     case 7: hipLaunchKernelGGL((splat_kernel<Co, true, true, false, FusedCfg>), sgrid, blk, 0, st, co, depth, io, a,
                                int(H), int(W), HW, g, nullptr); break;
     case 8: hipLaunchKernelGGL((splat_persist_kernel<Co, true, true, true>), dim3(persist_grid<Co, true>(sgrid.x)),
-                               blk, 0, st, co, depth, io, a, int(H), int(W), HW, g, stamps); break;
+                               dim3(FusedCfg::kThr), 0, st, co, depth, io, a, int(H), int(W), HW, g, stamps); break;
     case 9: hipLaunchKernelGGL((splat_persist_kernel<Co, true, true, false>), dim3(persist_grid<Co, true>(sgrid.x)),
-                               blk, 0, st, co, depth, io, a, int(H), int(W), HW, g, nullptr); break;
+                               dim3(FusedCfg::kThr), 0, st, co, depth, io, a, int(H), int(W), HW, g, nullptr); break;
 #define FV(CFG) hipLaunchKernelGGL((splat_kernel<Co, true, true, false, CFG>), sgrid, dim3(CFG::kThr), 0, st, co, depth, \
                                    io, a, int(H), int(W), HW, g, nullptr)
     case 10: FV(SplitCfg); break;                      // 512 threads, 2 targets in flight, 4 WG / CU
