@@ -268,12 +268,15 @@ def _stack_params(kind, params: List):
 
 
 def augment_flow_batch(img0, img0_depth, img1, img1_depth, flow01, back_flow01, kind, params: List,
-                       fw: Optional[FW] = None, specials: Optional[Tuple[torch.Tensor, torch.Tensor]] = None):
+                       fw: Optional[FW] = None, specials: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+                       inpaint_fn=None):
     """augment_flow (preprocess.py:107-182) over a batch: every tensor [B,...],
     ``params`` the per-image draws of draw_augment_params.  Returns (set1, set2,
     kind, specials) like the reference (specials None for kinds < 5).
-    ``specials`` optionally supplies the (special, back_special) flows."""
+    ``specials`` optionally supplies the (special, back_special) flows;
+    ``inpaint_fn`` replaces the hole-fill (default ops.inpaint)."""
     fw = fw or FW()
+    inpaint_ = inpaint_fn or inpaint
     cf, bf = ConcatFlow(), BackFlow()
     B, _, h, w = img0.shape
     dev = img0.device
@@ -286,10 +289,10 @@ def augment_flow_batch(img0, img0_depth, img1, img1_depth, flow01, back_flow01, 
         a0_flow, _ = cf(bsf, sf, flow01, img0_depth)
         a1_flow, _ = cf(flow01, back_flow01, sf, img1_depth)
         a0_all, valid, coll = fw(torch.cat((img0, img0_depth), 1), sf, img0_depth)
-        a0 = inpaint(a0_all[:, 0:3], valid, coll)
+        a0 = inpaint_(a0_all[:, 0:3], valid, coll)
         a0_depth = fix_warped_depth(a0_all[:, 3:4])
         a1_all, valid, coll = fw(torch.cat((img1, img1_depth), 1), sf, img1_depth)
-        a1 = inpaint(a1_all[:, 0:3], valid, coll)
+        a1 = inpaint_(a1_all[:, 0:3], valid, coll)
         a1_depth = fix_warped_depth(a1_all[:, 3:4])
         back_a0_flow, _ = bf(a0_flow, a0_depth)
         back_a1_flow, _ = bf(a1_flow, img0_depth)
@@ -354,12 +357,19 @@ class PreprocessPlusAugment(nn.Module):
     """preprocess.py:329-506: first-stage warps of one image (7 FW calls, 5
     hole-fills) into the 44-channel group, then 5 x 12 augmentations."""
 
-    def __init__(self, device):
+    def __init__(self, device, inpaint_fn=None, writer_workers: int = 0, compresslevel: int = 6):
+        """``inpaint_fn`` replaces utils.inpaint (default: the GPU hole-fill,
+        ops.inpaint); ``writer_workers`` > 0 writes the npz files from a
+        thread pool (NpzWriter) that overlaps the copies and the zlib work
+        with the GPU; ``compresslevel`` is the zip deflate level (6 =
+        np.savez_compressed's)."""
         super().__init__()
         self.device = device
         self.fw = FW(device)
         self.cf = ConcatFlow(device)
         self.bf = BackFlow(device)
+        self.inpaint_fn = inpaint_fn or inpaint
+        self.writer = NpzWriter(writer_workers, compresslevel) if writer_workers > 0 else None
 
     # -- the first stage, batched: img0 [B,3,H,W], img0_depth [B,1,H,W] (raw), params per image
     def stage_one(self, img0, img0_depth, params: List[Dict]):
@@ -377,7 +387,7 @@ class PreprocessPlusAugment(nn.Module):
         img1_depth = img1_depth * img1_valid
         back_flow01 = back_flow01 * img1_valid
         img1_depth = fix_warped_depth(img1_depth)
-        img1 = inpaint(img1, img1_valid, coll)                                         # :366
+        img1 = self.inpaint_fn(img1, img1_valid, coll)                                         # :366
 
         # :372-373 (and :385-387 below): the ego-motion flow plane is kept (it
         # is a group output); the warp derives the same flow in-kernel and
@@ -391,7 +401,7 @@ class PreprocessPlusAugment(nn.Module):
         img2 = img2 * img2_valid
         img2_depth = img2_depth * img2_valid
         back_flow12 = back_flow12 * img2_valid
-        img2 = inpaint(img2, img2_valid, coll)
+        img2 = self.inpaint_fn(img2, img2_valid, coll)
         img2_depth = fix_warped_depth(img2_depth)
 
         flow03, _ = Convert.depth_to_random_flow(img0_depth, T1=T1)                    # :385
@@ -400,7 +410,7 @@ class PreprocessPlusAugment(nn.Module):
         img3 = img3 * img3_valid
         img3_depth = img3_depth * img3_valid
         back_flow03 = back_flow03 * img3_valid
-        img3 = inpaint(img3, img3_valid, coll)
+        img3 = self.inpaint_fn(img3, img3_valid, coll)
         img3_depth = fix_warped_depth(img3_depth)
 
         flow02, flow02_valid = cf(flow01, back_flow01, flow12, img1_depth)             # :400
@@ -410,7 +420,7 @@ class PreprocessPlusAugment(nn.Module):
         img2p = img2p * img2p_valid
         img2p_depth = img2p_depth * img2p_valid
         back_flow02p = back_flow02p * img2p_valid
-        img2p = inpaint(img2p, img2p_valid, coll)
+        img2p = self.inpaint_fn(img2p, img2p_valid, coll)
         img2p_depth = fix_warped_depth(img2p_depth)
 
         flow13, flow13_valid = cf(back_flow01, flow01, flow03, img1_depth)             # :414
@@ -421,7 +431,7 @@ class PreprocessPlusAugment(nn.Module):
         img3p = img3p * img3p_valid
         img3p_depth = img3p_depth * img3p_valid
         back_flow13p = back_flow13p * img3p_valid
-        img3p = inpaint(img3p, img3p_valid, coll)
+        img3p = self.inpaint_fn(img3p, img3p_valid, coll)
         img3p_depth = fix_warped_depth(img3p_depth)
 
         groups = [(img0, img0_depth, img1, img1_depth, flow01, back_flow01),           # :427-432
@@ -440,7 +450,8 @@ class PreprocessPlusAugment(nn.Module):
         for g, (imgA, dA, imgB, dB, fAB, bAB) in enumerate(groups):
             for a, kind in enumerate(schedule):
                 set1, set2, _, _ = augment_flow_batch(imgA, dA, imgB, dB, fAB, bAB, kind,
-                                                      [p["augment"][g][a] for p in params], self.fw)
+                                                      [p["augment"][g][a] for p in params], self.fw,
+                                                      inpaint_fn=self.inpaint_fn)
                 yield g, a, kind, torch.cat(set1[0:4], 1), torch.cat(set2[2:6], 1)
 
     def run_batch(self, seeds: Sequence[int], img0, img0_depth, is_stereo=False, out_dirs=None,
@@ -456,11 +467,13 @@ class PreprocessPlusAugment(nn.Module):
             d0 = Convert.disparity_to_depth(d0)
         group44, groups = self.stage_one(img0, d0, params)
         if out_dirs is not None:
-            save_group(out_dirs, group44)
+            save_group(out_dirs, group44, self.writer)
         if augment:
             for g, a, kind, d1, d2 in self.augment(groups, params, schedule):
                 if out_dirs is not None:
-                    save_augment(out_dirs, g, a, kind, d1, d2)
+                    save_augment(out_dirs, g, a, kind, d1, d2, self.writer)
+        if self.writer is not None:
+            self.writer.flush()
         return group44
 
     def forward(self, datas, output_dir, is_stereo=False, n_continuous=4):
@@ -482,29 +495,111 @@ class PreprocessPlusAugment(nn.Module):
             d0 = Convert.disparity_to_depth(d0)
         os.makedirs(output_dir, exist_ok=True)
         group44, groups = self.stage_one(img0, d0, params)
-        save_group([output_dir], group44)
+        save_group([output_dir], group44, self.writer)
         for g, a, kind, d1, d2 in self.augment(groups, params):
-            save_augment([output_dir], g, a, kind, d1, d2)
+            save_augment([output_dir], g, a, kind, d1, d2, self.writer)
+        if self.writer is not None:
+            self.writer.flush()
 
 
 # ---------------------------------------------------------------- npz writer
-def save_group(out_dirs: Sequence[str], group44: torch.Tensor) -> None:
+def write_npz(path: str, compresslevel: int = 6, **arrays) -> None:
+    """np.savez_compressed's file (a deflated zip of .npy members, read back
+    by np.load) with a chosen zlib level; level 6 is numpy's own."""
+    import zipfile
+    from numpy.lib import format as npformat
+    with zipfile.ZipFile(path, mode="w", compression=zipfile.ZIP_DEFLATED, compresslevel=compresslevel,
+                         allowZip64=True) as zf:
+        for k, v in arrays.items():
+            with zf.open(k + ".npy", mode="w", force_zip64=True) as f:
+                npformat.write_array(f, np.asanyarray(v), allow_pickle=False)
+
+
+class NpzWriter:
+    """The npz files of preprocess.py:446, :471-476 written off the GPU's
+    critical path: each save copies the tensor to pinned host memory on the
+    current stream (non-blocking) behind an event, and a thread pool waits
+    for the event, then deflates and writes (zlib releases the GIL, so the
+    workers compress in parallel).  Pending bytes are capped: a save blocks
+    while more than ``max_pending_bytes`` wait to be written."""
+
+    def __init__(self, workers: int = 16, compresslevel: int = 6, max_pending_bytes: int = 8 << 30):
+        import threading
+        from concurrent.futures import ThreadPoolExecutor
+        self.pool = ThreadPoolExecutor(max_workers=workers, thread_name_prefix="npz")
+        self.level = compresslevel
+        self.cap = max_pending_bytes
+        self.pending = 0
+        self.cv = threading.Condition()
+        self.futures = []
+        self.bytes_written = 0
+
+    def _host(self, t):
+        if isinstance(t, torch.Tensor) and t.is_cuda:
+            h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+            h.copy_(t, non_blocking=True)
+            return h
+        return t
+
+    def save(self, path: str, **arrays) -> None:
+        nbytes = sum(int(t.numel() * t.element_size()) for t in arrays.values() if isinstance(t, torch.Tensor))
+        with self.cv:
+            while self.pending > 0 and self.pending + nbytes > self.cap:
+                self.cv.wait()
+            self.pending += nbytes
+        host = {k: self._host(v) for k, v in arrays.items()}
+        ev = torch.cuda.Event() if any(isinstance(v, torch.Tensor) and v.is_pinned() for v in host.values()) else None
+        if ev is not None:
+            ev.record()
+
+        def job():
+            try:
+                if ev is not None:
+                    ev.synchronize()
+                write_npz(path, self.level, **{k: (v.numpy() if isinstance(v, torch.Tensor) else v)
+                                               for k, v in host.items()})
+            finally:
+                with self.cv:
+                    self.pending -= nbytes
+                    self.bytes_written += nbytes
+                    self.cv.notify_all()
+        self.futures.append(self.pool.submit(job))
+
+    def flush(self) -> None:
+        """Wait for every pending file; re-raise the first write error."""
+        futs, self.futures = self.futures, []
+        for f in futs:
+            f.result()
+
+    def close(self) -> None:
+        self.flush()
+        self.pool.shutdown()
+
+
+def save_group(out_dirs: Sequence[str], group44: torch.Tensor, writer: Optional[NpzWriter] = None) -> None:
     """group.npz, key img_depth_flow = [44,H,W] (preprocess.py:434-447)."""
-    arr = group44.detach().cpu().numpy()
-    for d, x in zip(out_dirs, arr):
-        assert x.shape[0] == 44, "wrong data shape"
+    assert group44.shape[1] == 44, "wrong data shape"
+    for d, x in zip(out_dirs, group44.detach()):
         os.makedirs(d, exist_ok=True)
-        np.savez_compressed(os.path.join(d, "group.npz"), img_depth_flow=x)
+        path = os.path.join(d, "group.npz")
+        if writer is not None:
+            writer.save(path, img_depth_flow=x)
+        else:
+            np.savez_compressed(path, img_depth_flow=x.cpu().numpy())
 
 
-def save_augment(out_dirs: Sequence[str], g: int, a: int, kind: int, d1: torch.Tensor, d2: torch.Tensor) -> None:
+def save_augment(out_dirs: Sequence[str], g: int, a: int, kind: int, d1: torch.Tensor, d2: torch.Tensor,
+                 writer: Optional[NpzWriter] = None) -> None:
     """{g}_{a}_1.npz / {g}_{a}_2.npz, keys img_depth_flow [8,H,W] and
     augment_flow_type (preprocess.py:462-476)."""
-    a1, a2 = d1.detach().cpu().numpy(), d2.detach().cpu().numpy()
-    for d, x1, x2 in zip(out_dirs, a1, a2):
-        assert x1.shape[0] == 8 and x2.shape[0] == 8
-        np.savez_compressed(os.path.join(d, f"{g}_{a}_1.npz"), img_depth_flow=x1, augment_flow_type=kind)
-        np.savez_compressed(os.path.join(d, f"{g}_{a}_2.npz"), img_depth_flow=x2, augment_flow_type=kind)
+    assert d1.shape[1] == 8 and d2.shape[1] == 8
+    for d, x1, x2 in zip(out_dirs, d1.detach(), d2.detach()):
+        for k, x in ((1, x1), (2, x2)):
+            path = os.path.join(d, f"{g}_{a}_{k}.npz")
+            if writer is not None:
+                writer.save(path, img_depth_flow=x, augment_flow_type=np.array(kind))
+            else:
+                np.savez_compressed(path, img_depth_flow=x.cpu().numpy(), augment_flow_type=kind)
 
 
 # ---------------------------------------------------------------- driver (preprocess.py:508-561)

@@ -423,6 +423,47 @@ def make_config1_cases(ref_fw, Convert, utils_mod):
     return cases
 
 
+def make_ppa_forward_cases(utils_mod, ref_fw, Convert):
+    """The whole of PreprocessPlusAugment.forward for one small image: the
+    reference's text slices preprocess.py:24-182 (SpecialFlow, augment_flow),
+    :301-326 (ConcatFlow, BackFlow) and :329-476 (forward through the last
+    augment save) exec'd with the oracle as fw_cuda and the recording cv2
+    (its inpaint returns the uint8 cast unchanged).  The slice needs one
+    repair: :463 leaves its parenthesis open (the SyntaxError that makes the
+    file unparseable); the generator closes it.  Every
+    file forward writes -- group.npz and the 120 {g}_{a}_{1,2}.npz -- is
+    stored (16 x 24 pixels keeps the fixture small)."""
+    import tempfile
+    import torch.nn as nn
+    lines = open(os.path.join(REF, "preprocess.py")).read().split("\n")
+    assert lines[462].rstrip().endswith("axis=0"), lines[462]
+    body = lines[328:476]
+    body[462 - 328] = lines[462] + ")"  # the missing parenthesis of :463
+    ns = dict(torch=torch, nn=nn, np=np, os=os, sys=sys, time=__import__("time"), math=math,
+              utils=utils_mod, FW=ref_fw.FW, Convert=Convert, device="cpu")
+    for a, b in ((301, 326), (24, 182)):
+        exec(compile("\n".join(lines[a - 1:b]), os.path.join(REF, "preprocess.py"), "exec"), ns)
+    exec(compile("\n".join(body), os.path.join(REF, "preprocess.py"), "exec"), ns)
+    h, w, seed = 16, 24, 4711
+    raw = synth_depth(h, w, seed)
+    img0 = torch.from_numpy(synth_rgb(h, w, seed))
+    ppa = ns["PreprocessPlusAugment"]("cpu")
+    cases = {"seed": np.array(seed), "raw_depth": raw, "img0": img0.numpy()}
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "img")
+        utils_mod.set_seed(seed)
+        ppa((img0, torch.from_numpy(raw.copy()).unsqueeze(0)), out, False)
+        cases["group"] = np.load(os.path.join(out, "group.npz"))["img_depth_flow"]
+        for g in range(5):
+            for a in range(12):
+                for k in (1, 2):
+                    z = np.load(os.path.join(out, f"{g}_{a}_{k}.npz"))
+                    cases[f"aug/{g}_{a}_{k}"] = z["img_depth_flow"]
+                    cases[f"type/{g}_{a}_{k}"] = z["augment_flow_type"]
+        assert len(os.listdir(out)) == 121
+    return cases
+
+
 def main():
     ref_fw = load_reference_fw()
     geometry_mod = load_reference_geometry()
@@ -433,6 +474,14 @@ def main():
         c1 = make_config1_cases(ref_fw, Convert, utils_mod)
         np.savez_compressed(os.path.join(HERE, "config1.npz"), **c1)
         print("config1.npz", os.path.getsize(os.path.join(HERE, "config1.npz")), "bytes")
+        return
+    if sys.argv[1:] == ["ppa_forward"]:  # only the per-image forward fixture
+        ref_inpaint, rec = load_reference_inpaint()
+        utils_mod.inpaint = lambda img, valid, coll: ref_inpaint(img.as_subclass(_CpuImage), valid, coll).as_subclass(
+            torch.Tensor)
+        pf = make_ppa_forward_cases(utils_mod, ref_fw, Convert)
+        np.savez_compressed(os.path.join(HERE, "ppa_forward.npz"), **pf)
+        print("ppa_forward.npz", os.path.getsize(os.path.join(HERE, "ppa_forward.npz")), "bytes")
         return
     op = make_op_cases()
     np.savez_compressed(os.path.join(HERE, "fw_op.npz"), **op)

@@ -1,7 +1,18 @@
-"""Time the batched PreprocessPlusAugment on the GPU (no npz writing): the
-first stage (7 FW calls + 5 hole-fills per image) and the 5 x 12 augment loop
-(45 special-flow augmentations x (6 FW + 2 hole-fills)), B images per call."""
+"""Time the batched PreprocessPlusAugment on the GPU: the first stage (7 FW
+calls + 5 hole-fills per image) and the 5 x 12 augment loop (45 special-flow
+augmentations x (6 FW + 2 hole-fills)), B images per call, with or without
+writing the 121 npz files per image.
+
+usage: python tools/pipeline_time.py [B H W] [--save MODE ...] [--dir D]
+  MODE: none (compute only), sync (np.savez_compressed in the caller, the
+  reference's way, preprocess.py:446/:471), poolN:L (NpzWriter with N threads
+  at zlib level L; 6 = numpy's level).
+"""
+import argparse
+import os
+import shutil
 import sys
+import tempfile
 import time
 
 import torch
@@ -9,19 +20,42 @@ import torch
 sys.path.insert(0, __file__.rsplit("/tools/", 1)[0])
 from opticalflowfromdepth_amd import preprocess as pp, synth  # noqa: E402
 
-B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
-H, W = (int(sys.argv[2]), int(sys.argv[3])) if len(sys.argv) > 3 else (768, 1024)
+ap = argparse.ArgumentParser()
+ap.add_argument("shape", nargs="*", type=int, default=[64, 768, 1024])
+ap.add_argument("--save", nargs="*", default=["none"])
+ap.add_argument("--dir", default=None)
+ap.add_argument("--no-augment", action="store_true")
+args = ap.parse_args()
+B, H, W = (args.shape + [64, 768, 1024][len(args.shape):])[:3]
 dev = torch.device("cuda:0")
 seeds = [12345 + i for i in range(B)]
 img0 = synth.synthetic_rgb(seeds, H, W, dev)
 depth = synth.synthetic_depth(seeds, H, W, dev, dtype=torch.float64)
-ppa = pp.PreprocessPlusAugment(dev)
-ppa.run_batch(seeds[:2], img0[:2], depth[:2], augment=False)  # warm-up
-for aug in (False, True):
+pp.PreprocessPlusAugment(dev).run_batch(seeds[:2], img0[:2], depth[:2], augment=False)  # warm-up
+root = args.dir or tempfile.gettempdir()
+for mode in args.save:
+    workers, level = 0, 6
+    if mode.startswith("pool"):
+        n, level = mode[4:].split(":")
+        workers, level = int(n), int(level)
+    ppa = pp.PreprocessPlusAugment(dev, writer_workers=workers, compresslevel=level)
+    out = None
+    if mode != "none":
+        base = tempfile.mkdtemp(prefix="ppa_", dir=root)
+        out = [os.path.join(base, f"img{i}") for i in range(B)]
     torch.cuda.synchronize()
     t = time.perf_counter()
-    ppa.run_batch(seeds, img0, depth, augment=aug)
+    ppa.run_batch(seeds, img0, depth, out_dirs=out, augment=not args.no_augment)
     torch.cuda.synchronize()
     el = time.perf_counter() - t
-    print(f"{'stage one + 60 augmentations' if aug else 'stage one only'}: B={B} {H}x{W}: {el:.3f} s, "
-          f"{B / el:.2f} images/s", flush=True)
+    size = 0
+    if out is not None:
+        size = sum(os.path.getsize(os.path.join(d, f)) for d in out for f in os.listdir(d))
+        nfiles = sum(len(os.listdir(d)) for d in out)
+        shutil.rmtree(base)
+    what = "stage one only" if args.no_augment else "stage one + 60 augmentations"
+    print(f"{what}, save={mode}: B={B} {H}x{W}: {el:.3f} s, {B / el:.3f} images/s"
+          + (f", {nfiles} files, {size / 1e9:.2f} GB written ({size / el / 1e9:.2f} GB/s)" if out else ""),
+          flush=True)
+    if ppa.writer is not None:
+        ppa.writer.close()
