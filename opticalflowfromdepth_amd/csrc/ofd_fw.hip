@@ -747,6 +747,25 @@ __global__ __launch_bounds__(kWarpThreads) void bin_kernel(Coords co, const floa
 // XCD sees every image (whole images per XCD left the XCDs holding the
 // heavier ego-motion images running ~60 us after the rest had drained).
 // Placement only affects speed, never results.
+//
+// Inside a band the heavy tiles of every image come first (longest job
+// first): the warp clamps out-of-image targets onto the border
+// (fw.py:37-42), so border tiles collect every source that leaves the image
+// and take up to 5x a median tile; dequeued last they set the drain tail.
+// OFD_TILE_ORDER: 0 = plain band-major, 1 = corner tiles first, 3 = border
+// tiles first.
+#ifndef OFD_TILE_ORDER
+#define OFD_TILE_ORDER 0
+#endif
+// heavy columns of tile row r: 0 = none, 1 = the two end columns, 2 = all
+[[maybe_unused]] __device__ __forceinline__ int heavy_kind(int r, const TileGeom &g) {
+    const bool edge_row = r == 0 || r == g.tilesY - 1;
+    if constexpr (OFD_TILE_ORDER == 1) return edge_row ? 1 : 0;
+    else if constexpr (OFD_TILE_ORDER == 3) return edge_row ? 2 : 1;
+    else return 0;
+}
+[[maybe_unused]] __device__ __forceinline__ int n_heavy(int kind, int tx) { return kind == 0 ? 0 : kind == 2 ? tx : (tx > 1 ? 2 : 1); }
+
 __device__ __forceinline__ void band_major_tile(unsigned lin, int nimg, const TileGeom &g, int &bl, int &tile) {
     unsigned start = 0;
     for (int k = 0; k < 8; ++k) {
@@ -754,9 +773,30 @@ __device__ __forceinline__ void band_major_tile(unsigned lin, int nimg, const Ti
         const unsigned per_img = unsigned(r1 - r0) * unsigned(g.tilesX);
         const unsigned cnt = per_img * unsigned(nimg);
         if (lin < start + cnt || k == 7) {
-            const unsigned idx = lin - start;
-            bl = int(idx / per_img);
-            tile = r0 * g.tilesX + int(idx - unsigned(bl) * per_img);
+            unsigned idx = lin - start;
+            if constexpr (OFD_TILE_ORDER == 0) {
+                bl = int(idx / per_img);
+                tile = r0 * g.tilesX + int(idx - unsigned(bl) * per_img);
+            } else {
+                unsigned nh = 0;
+                for (int r = r0; r < r1; ++r) nh += unsigned(n_heavy(heavy_kind(r, g), g.tilesX));
+                const bool heavy = idx < nh * unsigned(nimg);
+                const unsigned per = heavy ? nh : per_img - nh;
+                if (!heavy) idx -= nh * unsigned(nimg);
+                bl = int(idx / per);
+                int kk = int(idx - unsigned(bl) * per);
+                tile = r0 * g.tilesX;
+                for (int r = r0; r < r1; ++r) {
+                    const int kind = heavy_kind(r, g), nhr = n_heavy(kind, g.tilesX);
+                    const int n = heavy ? nhr : g.tilesX - nhr;
+                    if (kk < n) {
+                        const int col = heavy ? (kind == 2 ? kk : (kk == 0 ? 0 : g.tilesX - 1)) : (kind == 0 ? kk : 1 + kk);
+                        tile = r * g.tilesX + col;
+                        break;
+                    }
+                    kk -= n;
+                }
+            }
             return;
         }
         start += cnt;
@@ -1417,6 +1457,10 @@ unsigned resident_slots(K kernel, int threads) {
             hipSuccess ||
         cus <= 0 || per <= 0)
         return 1024u;
+    if (const char *e = getenv("OFD_SPLAT_WG_PER_CU")) {  // probe knob: workgroups per CU of the grid
+        const int v = atoi(e);
+        if (v > 0) per = v;
+    }
     return unsigned(cus) * unsigned(per);
 }
 
