@@ -1307,17 +1307,24 @@ unsigned tail_grid() {
     return v;
 }
 
-// Per-shape layer statistics of the previous call, read back without ever
+// Per-shape layer statistics of recent calls, read back without ever
 // blocking the host: every call enqueues an asynchronous copy of its layer
 // histogram and depth into pinned memory behind an event; a later call uses
 // them (to size its grids and the number of layer launches) only once that
-// event has completed.  They steer launch sizes only, never results.
+// event has completed.  They steer launch sizes only, never results.  The
+// view is the elementwise maximum over the last kHistory completed copies: a
+// caller that alternates shallow and deep fills at one shape (the pipeline's
+// flip / rotation / shear augmentations) then launches the deep calls' layers
+// -- an unneeded layer launch costs ~1.6 us, a layer left to the one-
+// workgroup-per-CU tail kernel several times a launched layer.
 struct LaggedStats {
+    static constexpr size_t kHistory = 8;
     std::mutex mu;
     unsigned *pinned = nullptr;  // [kMaxBins + 1]: hist, then the depth (meta[0])
     hipEvent_t ev = nullptr;
     bool pending = false;
-    std::vector<unsigned> hist;  // last completed copy
+    std::vector<std::vector<unsigned>> recent;  // completed copies, oldest first; [nbins] hist + depth
+    std::vector<unsigned> hist;                 // elementwise max over `recent`
     unsigned lmax = 0, ring = 0;
     bool valid = false;
     struct View {
@@ -1328,8 +1335,17 @@ struct LaggedStats {
     View snapshot(int nbins, int nring) {
         std::lock_guard<std::mutex> lk(mu);
         if (pending && hipEventQuery(ev) == hipSuccess) {
-            hist.assign(pinned, pinned + nbins);
-            lmax = pinned[kMaxBins];
+            std::vector<unsigned> h(pinned, pinned + nbins);
+            h.push_back(pinned[kMaxBins]);
+            if (!recent.empty() && recent.back().size() != h.size()) recent.clear();
+            recent.push_back(std::move(h));
+            if (recent.size() > kHistory) recent.erase(recent.begin());
+            hist.assign(size_t(nbins), 0u);
+            lmax = 0;
+            for (const auto &r : recent) {
+                for (int k = 0; k < nbins; ++k) hist[size_t(k)] = std::max(hist[size_t(k)], r[size_t(k)]);
+                lmax = std::max(lmax, r.back());
+            }
             ring = 0;
             for (int k = 0; k < nring && k < nbins; ++k) ring += hist[size_t(k)];
             valid = true;

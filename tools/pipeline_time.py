@@ -25,9 +25,13 @@ ap.add_argument("shape", nargs="*", type=int, default=[64, 768, 1024])
 ap.add_argument("--save", nargs="*", default=["none"])
 ap.add_argument("--dir", default=None)
 ap.add_argument("--no-augment", action="store_true")
+ap.add_argument("--ip-schedule", default=None, help="L:T -> ofd_inpaint_set_schedule(L, T) (hole-fill launch knobs)")
 args = ap.parse_args()
 B, H, W = (args.shape + [64, 768, 1024][len(args.shape):])[:3]
 dev = torch.device("cuda:0")
+if args.ip_schedule:
+    from opticalflowfromdepth_amd import _native
+    _native.lib().ofd_inpaint_set_schedule(*(int(v) for v in args.ip_schedule.split(":")))
 seeds = [12345 + i for i in range(B)]
 img0 = synth.synthetic_rgb(seeds, H, W, dev)
 depth = synth.synthetic_depth(seeds, H, W, dev, dtype=torch.float64)
