@@ -21,15 +21,19 @@
 // Launches per chunk of images:
 //   PREP   one thread per pixel: keep mask (3x3 dilation of valid != coll),
 //          hole bits, out = float(uint8(img)) for every pixel.
-//   COLS   one thread per column: vertical distances to the nearest known /
-//          hole pixel (two sweeps).
+//   COLS   64 columns x 8 row segments per workgroup: vertical distances to
+//          the nearest known / hole pixel (two sweeps).
 //   ROWS   one wave per row (prefix / suffix scans): the row pass of both L1 distance transforms,
 //          the Chebyshev-radius test of the outer band; writes the per-pixel
 //          code (hole layer / band / ring layer / far) and initial T.
 //   SORT   chip-wide counting sort of ring pixels and holes by layer (LDS
-//          histograms, one scan, one host read of the layer counts).
-//   LAYERS one launch per outer-band layer and per hole layer, one thread
-//          per pixel of every image of the chunk.
+//          histograms, one scan, one scatter); the counts stay on the device.
+//   LAYERS one launch per outer-band layer and per hole layer over every
+//          image of the chunk, each reading its layer's size and offset from
+//          the device; a persistent tail kernel (grid barrier between layers)
+//          runs any layer deeper than the launches.  Grids and the number of
+//          launches come from recent calls' counts read back asynchronously
+//          (LaggedStats): the host never waits.
 //
 // Plain HIP for gfx950; FP contraction off so the float / double sequence is
 // the oracle's.

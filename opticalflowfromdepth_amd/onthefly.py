@@ -23,7 +23,7 @@ of DataParallel.  The flow network is a small stand-in with RAFT's interface
 out of scope.
 
 ``PairOps`` carries the three device ops; the CPU multi-rank test
-(tests/test_onthefly.py) swaps in CPU restatements from oracle/, the product
+(tests/test_onthefly.py) swaps in the CPU restatements kept under oracle/, the product
 default is the HIP path and fails loudly without it.
 """
 from __future__ import annotations

@@ -199,6 +199,14 @@ def inpaint(img: torch.Tensor, valid: torch.Tensor, collision: torch.Tensor, rad
     utils.py:137-142 drops are filled (Telea weights, layered marching; see
     include/ofd_inpaint.h); every pixel of the result is float32 of the
     uint8 cast of utils.py:148, on img's device, like the reference's return.
+
+    The fill values are NOT cv2's: holes are finalised in layers of equal L1
+    distance instead of cv2's one-at-a-time heap order.  The specified
+    divergence (tests/test_inpaint.py): on warped
+    random-RGB images 85 % of hole values differ from the sequential order,
+    mean 5.7 grey levels, p99 40; within 1-2 levels on smooth images.  Kept
+    pixels, the mask algebra and the cast are the reference's exactly.  The
+    call never blocks the host.
     """
     for x, n in ((img, "img"), (valid, "valid"), (collision, "collision")):
         if not isinstance(x, torch.Tensor):
