@@ -22,7 +22,12 @@
  *       divergence from cv2's sequential order: on
  *       warped random-RGB images 85 % of hole values differ, mean 5.7 grey
  *       levels, p99 40; within 1-2 levels on smooth images.
- *   ofd_inpaint_workspace_bytes
+ *   ofd_inpaint_telea_seq_f32
+ *       utils.inpaint, as above, with the fill in cv2's sequential order
+ *       (bit-exact against oracle/inpaint_oracle.c sequential mode, OpenCV's
+ *       icvCalcFMM / icvTeleaInpaintFMM restated): bucketed parallel fast
+ *       march + colours in dependency levels.
+ *   ofd_inpaint_workspace_bytes, ofd_inpaint_seq_workspace_bytes
  *       no reference counterpart (cv2 allocates its fast-marching state per
  *       call); caller-owned scratch, no initialisation needed.
  *   ofd_inpaint_set_schedule
@@ -59,6 +64,25 @@ size_t ofd_inpaint_workspace_bytes(int64_t B, int64_t H, int64_t W);
 int ofd_inpaint_telea_f32(const float *img, const float *valid, const float *collision, float *out,
                           int64_t B, int64_t C, int64_t H, int64_t W, int radius, void *workspace,
                           size_t workspace_bytes, void *stream);
+
+/* Bytes of workspace for ofd_inpaint_telea_seq_f32 over B images of H x W
+ * (about 40 bytes per padded pixel; any size of at least one image's share
+ * works, larger ones process more images per launch). */
+size_t ofd_inpaint_seq_workspace_bytes(int64_t B, int64_t H, int64_t W);
+
+/* utils.inpaint, batched, in cv2's exact order: the same arguments and
+ * conventions as ofd_inpaint_telea_f32, but the fill follows the sequential
+ * fast march of cv2.inpaint(..., INPAINT_TELEA) (utils.py:149) -- heap pops in
+ * (distance, push order), each pushed hole coloured from the pixels reached
+ * before it -- and is bit-exact against its CPU restatement
+ * oracle/inpaint_oracle.c (sequential mode).  cv2 itself is absent from the
+ * build image, so parity with OpenCV's binary is pinned only through that
+ * restatement of OpenCV's published source.  Requires H >= 2, W >= 2 and
+ * (H+2)(W+2) < 2^30 (OFD_FW_ETOOBIG).  Asynchronous on `stream`; never blocks
+ * the host. */
+int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float *collision, float *out,
+                              int64_t B, int64_t C, int64_t H, int64_t W, int radius, void *workspace,
+                              size_t workspace_bytes, void *stream);
 
 /* Diagnostics: launch_layers >= 0 launches exactly that many hole layers one
  * by one (the deep-tail kernel does the rest); thin_cap >= 0 sets the layer

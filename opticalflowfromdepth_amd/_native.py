@@ -48,6 +48,8 @@ SIGNATURES = {
     "ofd_fw_warp_ego_f64depth": ([_P, _I64] + [_P] * 6 + [_I64] * 3 + [_P, _SZ, _P], ctypes.c_int),
     "ofd_inpaint_workspace_bytes": ([_I64, _I64, _I64], _SZ),
     "ofd_inpaint_telea_f32": ([_P] * 4 + [_I64] * 4 + [ctypes.c_int, _P, _SZ, _P], ctypes.c_int),
+    "ofd_inpaint_seq_workspace_bytes": ([_I64, _I64, _I64], _SZ),
+    "ofd_inpaint_telea_seq_f32": ([_P] * 4 + [_I64] * 4 + [ctypes.c_int, _P, _SZ, _P], ctypes.c_int),
     "ofd_inpaint_set_schedule": ([ctypes.c_int, ctypes.c_int], ctypes.c_int),
 }
 

@@ -14,8 +14,9 @@ import sys
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(_HERE)
-SRCS = [os.path.join(_HERE, "csrc", f) for f in ("ofd_fw.hip", "ofd_inpaint.hip")]
-HDRS = [os.path.join(REPO, "include", f) for f in ("ofd_fw.h", "ofd_inpaint.h")]
+SRCS = [os.path.join(_HERE, "csrc", f) for f in ("ofd_fw.hip", "ofd_inpaint.hip", "ofd_inpaint_seq.hip")]
+HDRS = [os.path.join(REPO, "include", f) for f in ("ofd_fw.h", "ofd_inpaint.h")] + [
+    os.path.join(_HERE, "csrc", "ip_common.h")]
 OUT_DIR = os.path.join(_HERE, "_build")
 OUT = os.path.join(OUT_DIR, "libofd_fw.so")
 ARCH = os.environ.get("OFD_OFFLOAD_ARCH", "gfx950")

@@ -58,6 +58,8 @@
 
 namespace {
 
+#include "ip_common.h"
+
 // Diagnostic build only (tools/probe_ip.hip defines OFD_IP_STAMPS): thread 0
 // of the first block of each path of a hole-layer launch records shader-clock
 // stamps along the per-hole chain; the product build compiles them out.
@@ -72,7 +74,6 @@ __device__ __forceinline__ void ip_stamp(unsigned slot, unsigned k) {
 #define IP_STAMP(slot, k, cond) do { } while (0)
 #endif
 
-constexpr float T_FAR = 1.0e6f;
 // per-pixel code: bit 15 hole, bit 14 outer ring, bit 13 far known, low 13
 // bits the layer (holes: L1 distance to the known region, LAY_INF = none;
 // ring: L1 distance to the band); 0 = band (known, 4-adjacent to a hole)
@@ -109,18 +110,6 @@ IpWs carve(void *ws, int64_t G, int64_t HW) {
     p += align256(size_t(G) * size_t(HW) * 4);
     w.gcol = reinterpret_cast<uint32_t *>(p);
     return w;
-}
-
-// numpy float32 -> uint8 on x86 (utils.py:148): truncate through int32, keep the low byte
-__device__ __forceinline__ unsigned to_u8(float v) {
-    if (!(v > -2147483648.0f && v < 2147483648.0f)) return 0u;
-    return unsigned(int(v)) & 0xFFu;
-}
-
-// cv::saturate_cast<uchar>(float): round half to even, clamp
-__device__ __forceinline__ unsigned sat_u8(float v) {
-    const float r = __builtin_rintf(v);
-    return r < 0.f ? 0u : (r > 255.f ? 255u : unsigned(r));
 }
 
 // ---------------------------------------------------------------- PREP
@@ -473,33 +462,6 @@ __device__ __forceinline__ float tval(const Img &m, int y, int x, unsigned L, bo
     in = inside<kOuter>(m, y, x, L);
     if (in || y < 0 || x < 0 || y >= m.H || x >= m.W) return T_FAR;
     return m.T[int64_t(y) * m.W + x];
-}
-
-// FastMarching_solve (double), with cv2's flag cases
-__device__ __forceinline__ float fm_solve(float t1, bool in1, float t2, bool in2) {
-    const double a11 = t1, a22 = t2;
-    const double m12 = a11 < a22 ? a11 : a22;
-    double sol;
-    if (!in1) {
-        if (!in2) {
-            if (fabs(a11 - a22) >= 1.0)
-                sol = 1 + m12;
-            else
-                sol = (a11 + a22 + sqrt(double(2 - (a11 - a22) * (a11 - a22)))) * 0.5;
-        } else {
-            sol = 1 + a11;
-        }
-    } else if (!in2) {
-        sol = 1 + a22;
-    } else {
-        sol = 1 + m12;
-    }
-    return float(sol);
-}
-
-__device__ __forceinline__ float min4f(float a, float b, float c, float d) {
-    const float x = a < b ? a : b, y = c < d ? c : d;
-    return x < y ? x : y;
 }
 
 template <bool kOuter>

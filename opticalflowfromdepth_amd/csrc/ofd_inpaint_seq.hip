@@ -1,0 +1,710 @@
+// ofd_inpaint_seq.hip -- MI355X (gfx950) hole-fill in cv2's exact order.
+//
+// Replaces utils.inpaint (utils.py:136-151) with results equal to cv2's
+// sequential Telea fast march (cv2.inpaint(..., 3, cv2.INPAINT_TELEA), :149)
+// as restated by oracle/inpaint_oracle.c (sequential mode): the same pop
+// order, distances, and colours, bit for bit.
+//
+// cv2 pops the band pixel of least (T, push order) from a heap; each pop
+// gives its INSIDE 4-neighbours a distance (FastMarching_solve over the
+// neighbours reached so far), a colour (Telea's weighted window over the
+// pixels reached so far) and pushes them.  Two facts make that order
+// reproducible in parallel:
+//
+//  1. A pushed pixel's distance is at least the popped one's + 1/sqrt(2)
+//     (every reached neighbour of an INSIDE pixel is a heap member with
+//     T >= the current minimum, and FastMarching_solve adds >= 0.7071 to the
+//     smaller argument).  So the pops with T in [k/2, (k+1)/2) are exactly
+//     the heap's contents in that range when the range becomes the minimum:
+//     none of them pushes anything into its own range.  FMM runs one such
+//     bucket at a time: sort the bucket by (T, push order), let every pop
+//     claim its INSIDE neighbours (atomicMin over (pop rank, direction): the
+//     first claimant is the pusher, as in the serial loop), number the pushes
+//     in (rank, direction) order -- cv2's push order -- and solve their
+//     distances.  A push may read a neighbour pushed earlier in the same
+//     bucket, so the distances are iterated to a fixed point (the system is
+//     acyclic in push order, so a sweep with no change is the exact answer).
+//  2. Colours do not steer the march: T and the push order depend on the
+//     mask only.  With every pixel's push stamp known, a hole's colour reads
+//     exactly the holes of smaller stamp in its window (cv2's INSIDE test is
+//     "not pushed yet"), so COLOUR evaluates the holes in dependency levels
+//     (Kahn's algorithm: a hole runs once every earlier-stamped hole in its
+//     window has), all holes of a level in parallel.
+//
+// Launches per chunk of images (one workgroup per image for the two
+// sequential phases):
+//   PREP   per pixel: keep mask (utils.py:137-142), out = float(uint8(img)),
+//          inner stamps (INF = hole).
+//   INIT   one wave per padded row: frame, band (4-adjacent to a hole),
+//          outer ring (a hole within Chebyshev `range`), t, owner keys; band
+//          count per row.
+//   BAND   row offsets, then the band pixels in raster order (cv2 pushes them
+//          in that order with T = 0).
+//   FMM    per image: the outer march over the ring (icvCalcFMM with negate),
+//          its distances negated, then the inner march over the holes.
+//   COUNT  per pixel: earlier-stamped holes in the window; level-0 holes.
+//   COLOUR per image: Kahn levels, cv2's Telea colour per hole.
+//
+// Plain HIP for gfx950; FP contraction off so the float / double sequence is
+// the oracle's (and OpenCV's source's).
+
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+
+#include "ofd_fw.h"
+#include "ofd_inpaint.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+#include "ip_common.h"
+
+constexpr uint32_t INF = 0xFFFFFFFFu;
+constexpr int kThreads = 1024;  // FMM / COLOUR workgroup
+constexpr int kCap = 4096;      // bucket keys sorted in LDS; larger buckets merge in global memory
+constexpr int kMaxRange = 100;
+constexpr int kMeta = 8;  // per image: 0 band count, 1 pushes, 2 frontier count, 3 levels, 4 buckets, 5 error
+
+inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+// per-image arrays over the padded (H+2) x (W+2) grid (cv2's one-pixel KNOWN frame)
+struct SqWs {
+    uint32_t *sO;    // outer march stamps: INF = ring pixel not reached yet, else push seq (0 = never in heap)
+    uint32_t *sI;    // inner march stamps: INF = hole not reached yet, else push seq (0 = known)
+    uint32_t *own;   // FMM: claiming (rank * 4 + direction); COLOUR: pending dependencies
+    float *t;        // distances (cv2's t; 1e6 far)
+    uint32_t *logp;  // push log: pixel of push seq s (band first, raster order)
+    float *logt;     // push log: T of push seq s
+    uint64_t *k0;    // large-bucket sort buffers; COLOUR frontiers
+    uint64_t *k1;
+    uint32_t *rowc;  // band count / offset per padded row
+    uint32_t *meta;  // kMeta words per image
+    int64_t en, eh, ew;
+};
+
+size_t per_image_bytes(int64_t H, int64_t W) {
+    const size_t en = size_t(H + 2) * size_t(W + 2);
+    return align256(en * 4) * 6 + align256(en * 8) * 2 + align256(size_t(H + 2) * 4) + 256;
+}
+
+SqWs carve(void *ws, int64_t G, int64_t H, int64_t W) {
+    SqWs w;
+    w.eh = H + 2;
+    w.ew = W + 2;
+    w.en = w.eh * w.ew;
+    const size_t n4 = align256(size_t(G) * size_t(w.en) * 4), n8 = align256(size_t(G) * size_t(w.en) * 8);
+    char *p = static_cast<char *>(ws);
+    w.sO = reinterpret_cast<uint32_t *>(p), p += n4;
+    w.sI = reinterpret_cast<uint32_t *>(p), p += n4;
+    w.own = reinterpret_cast<uint32_t *>(p), p += n4;
+    w.t = reinterpret_cast<float *>(p), p += n4;
+    w.logp = reinterpret_cast<uint32_t *>(p), p += n4;
+    w.logt = reinterpret_cast<float *>(p), p += n4;
+    w.k0 = reinterpret_cast<uint64_t *>(p), p += n8;
+    w.k1 = reinterpret_cast<uint64_t *>(p), p += n8;
+    w.rowc = reinterpret_cast<uint32_t *>(p), p += align256(size_t(G) * size_t(w.eh) * 4);
+    w.meta = reinterpret_cast<uint32_t *>(p);
+    return w;
+}
+
+// One image's view of the workspace
+struct Img {
+    uint32_t *sO, *sI, *own, *logp, *rowc, *meta;
+    float *t, *logt;
+    uint64_t *k0, *k1;
+    int64_t en;
+    int eh, ew;
+};
+
+__device__ __forceinline__ Img image(const SqWs &w, int64_t bl) {
+    Img m;
+    m.sO = w.sO + bl * w.en;
+    m.sI = w.sI + bl * w.en;
+    m.own = w.own + bl * w.en;
+    m.t = w.t + bl * w.en;
+    m.logp = w.logp + bl * w.en;
+    m.logt = w.logt + bl * w.en;
+    m.k0 = w.k0 + bl * w.en;
+    m.k1 = w.k1 + bl * w.en;
+    m.rowc = w.rowc + bl * w.eh;
+    m.meta = w.meta + bl * kMeta;
+    m.en = w.en;
+    m.eh = int(w.eh);
+    m.ew = int(w.ew);
+    return m;
+}
+
+// Workgroup barrier whose global writes are visible to every thread of the
+// workgroup afterwards: release at agent scope (atomics and stores reach L2),
+// barrier, acquire at agent scope (the CU's vector L1 is invalidated, so no
+// thread reads a line cached before another thread's update).
+__device__ __forceinline__ void sync_all() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
+// Exclusive scan of one value per thread over the 1024-thread workgroup.
+__device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t &total, uint32_t *scr /* [40] LDS */) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint32_t incl = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(incl, d);
+        if (lane >= d) incl += o;
+    }
+    if (lane == 63) scr[wave] = incl;
+    __syncthreads();
+    if (tid < 64) {
+        const uint32_t w = tid < kThreads / 64 ? scr[tid] : 0u;
+        uint32_t wi = w;
+#pragma unroll
+        for (int d = 1; d < 16; d <<= 1) {
+            const uint32_t o = __shfl_up(wi, d);
+            if (lane >= d) wi += o;
+        }
+        if (tid < kThreads / 64) scr[16 + tid] = wi - w;
+        if (tid == kThreads / 64 - 1) scr[32] = wi;
+    }
+    __syncthreads();
+    const uint32_t r = incl - v + scr[16 + wave];
+    total = scr[32];
+    __syncthreads();
+    return r;
+}
+
+// ---------------------------------------------------------------- PREP
+// utils.py:137-142: M = valid != coll; M' = 3x3 max (border excluded);
+// P = M' == M; H' = uint8(valid * P); fill where 1 - H' != 0.  Writes the
+// uint8 cast of every channel (utils.py:148) and sI (INF = hole, 0 = known)
+// at the padded position.
+__global__ __launch_bounds__(256) void sq_prep_kernel(const float *__restrict__ img, const float *__restrict__ valid,
+                                                      const float *__restrict__ coll, float *__restrict__ out,
+                                                      SqWs w, int C, int H, int W, int64_t b0) {
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63), y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (x >= W || y >= H) return;
+    const int64_t HW = int64_t(H) * W, bl = blockIdx.z, b = b0 + bl;
+    const float *v = valid + b * HW, *cl = coll + b * HW;
+    const int64_t p = int64_t(y) * W + x;
+    unsigned mp = 0;
+    for (int dy = -1; dy <= 1; ++dy)
+        for (int dx = -1; dx <= 1; ++dx) {
+            const int yy = y + dy, xx = x + dx;
+            if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
+                const int64_t q = int64_t(yy) * W + xx;
+                mp |= v[q] != cl[q] ? 1u : 0u;
+            }
+        }
+    const unsigned M = v[p] != cl[p] ? 1u : 0u;
+    const unsigned P = mp == M ? 1u : 0u;
+    const unsigned hp = to_u8(v[p] * float(P));
+    w.sI[bl * w.en + int64_t(y + 1) * w.ew + (x + 1)] = hp != 1u ? INF : 0u;
+    const float *ib = img + b * int64_t(C) * HW;
+    float *ob = out + b * int64_t(C) * HW;
+    for (int c = 0; c < C; ++c) ob[c * HW + p] = float(to_u8(ib[c * HW + p]));
+}
+
+// ---------------------------------------------------------------- INIT
+// One wave per padded row.  Holes are read by coordinates (the frame is never
+// a hole), so the frame entries this kernel writes are never read here.
+__global__ __launch_bounds__(256) void sq_init_kernel(SqWs w, int range) {
+    const int lane = threadIdx.x & 63, i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const Img m = image(w, blockIdx.y);
+    if (i >= m.eh) return;
+    const int eh = m.eh, ew = m.ew;
+    auto hole = [&](int y, int x) -> bool {
+        return y > 0 && x > 0 && y < eh - 1 && x < ew - 1 && m.sI[int64_t(y) * ew + x] == INF;
+    };
+    uint32_t nband = 0;
+    for (int j0 = 0; j0 < ew; j0 += 64) {
+        const int j = j0 + lane;
+        bool band = false;
+        if (j < ew) {
+            const int64_t p = int64_t(i) * ew + j;
+            const bool frame = i == 0 || j == 0 || i == eh - 1 || j == ew - 1;
+            bool ring = false;
+            if (!frame && !hole(i, j)) {
+                band = hole(i - 1, j) || hole(i + 1, j) || hole(i, j - 1) || hole(i, j + 1);
+                if (!band)
+                    for (int y = i - range; y <= i + range && !ring; ++y)
+                        for (int x = j - range; x <= j + range; ++x)
+                            if (hole(y, x)) {
+                                ring = true;
+                                break;
+                            }
+            }
+            if (frame) m.sI[p] = 0u;
+            m.sO[p] = ring ? INF : 0u;
+            m.t[p] = band ? 0.f : T_FAR;
+            m.own[p] = INF;
+        }
+        nband += __popcll(__ballot(band));
+    }
+    if (lane == 0) m.rowc[i] = nband;
+}
+
+// Row offsets of the band (exclusive scan over rows), one workgroup per image.
+__global__ __launch_bounds__(kThreads) void sq_band_scan_kernel(SqWs w) {
+    __shared__ uint32_t scr[40];
+    const Img m = image(w, blockIdx.x);
+    uint32_t carry = 0;
+    for (int i0 = 0; i0 < m.eh; i0 += kThreads) {
+        const int i = i0 + threadIdx.x;
+        const uint32_t v = i < m.eh ? m.rowc[i] : 0u;
+        uint32_t tot;
+        const uint32_t ex = block_scan(v, tot, scr);
+        if (i < m.eh) m.rowc[i] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) {
+        for (int k = 0; k < kMeta; ++k) m.meta[k] = 0u;
+        m.meta[0] = carry;
+    }
+}
+
+// Band pixels in raster order into the push log (cv2's Heap->Add, T = 0).
+__global__ __launch_bounds__(256) void sq_band_write_kernel(SqWs w) {
+    const int lane = threadIdx.x & 63, i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const Img m = image(w, blockIdx.y);
+    if (i >= m.eh) return;
+    uint32_t off = m.rowc[i];
+    for (int j0 = 0; j0 < m.ew; j0 += 64) {
+        const int j = j0 + lane;
+        const int64_t p = int64_t(i) * m.ew + j;
+        const bool band = j < m.ew && m.t[p] == 0.f;
+        const uint64_t bal = __ballot(band);
+        if (band) {
+            const uint32_t s = off + __popcll(bal & ((uint64_t(1) << lane) - 1));
+            m.logp[s] = uint32_t(p);
+            m.logt[s] = 0.f;
+        }
+        off += __popcll(bal);
+    }
+}
+
+// ---------------------------------------------------------------- FMM
+struct FmmLds {
+    uint64_t keys[kCap];
+    uint32_t scr[40];
+    uint32_t tmin, tmax, chg;
+};
+
+__device__ __forceinline__ uint32_t bucket_of(float T) { return uint32_t(T * 2.0f); }
+
+// distance of padded pixel p pushed with seq s: FastMarching_solve over the
+// neighbours reached before it (stamp < s); cv2's fm order (up/left,
+// down/left, up/right, down/right)
+__device__ __forceinline__ float fm_dist_seq(const uint32_t *st, const float *t, int64_t p, int ew, uint32_t s) {
+    const int64_t nu = p - ew, nd = p + ew, nl = p - 1, nr = p + 1;
+    const bool iu = st[nu] >= s, id = st[nd] >= s, il = st[nl] >= s, ir = st[nr] >= s;
+    const float tu = iu ? T_FAR : t[nu], td = id ? T_FAR : t[nd], tl = il ? T_FAR : t[nl], tr = ir ? T_FAR : t[nr];
+    return min4f(fm_solve(tu, iu, tl, il), fm_solve(td, id, tl, il), fm_solve(tu, iu, tr, ir),
+                 fm_solve(td, id, tr, ir));
+}
+
+// bitonic sort of keys[0, m) in LDS, m a power of two
+__device__ void lds_bitonic(uint64_t *s, int m) {
+    for (int k = 2; k <= m; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < m; i += kThreads) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const uint64_t a = s[i], b = s[ixj];
+                    const bool up = (i & k) == 0;
+                    if ((a > b) == up) {
+                        s[i] = b;
+                        s[ixj] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+}
+
+__device__ __forceinline__ uint32_t lower_bound64(const uint64_t *a, uint32_t n, uint64_t key) {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a[mid] < key)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+
+// Sort n > kCap keys held in g[0, n): LDS-sorted runs of kCap, then merge
+// passes between g and h (unique keys: each element's place is its rank in
+// its own run plus its rank in the partner run).  Returns the buffer that
+// holds the result.
+__device__ uint64_t *global_sort(uint64_t *g, uint64_t *h, uint32_t n, FmmLds &L) {
+    for (uint32_t r0 = 0; r0 < n; r0 += kCap) {
+        const uint32_t len = min(uint32_t(kCap), n - r0);
+        for (int i = threadIdx.x; i < kCap; i += kThreads) L.keys[i] = uint32_t(i) < len ? g[r0 + i] : ~uint64_t(0);
+        __syncthreads();
+        lds_bitonic(L.keys, kCap);
+        for (int i = threadIdx.x; uint32_t(i) < len; i += kThreads) g[r0 + i] = L.keys[i];
+        sync_all();
+    }
+    uint64_t *src = g, *dst = h;
+    for (uint32_t wdt = kCap; wdt < n; wdt <<= 1) {
+        for (uint32_t i = threadIdx.x; i < n; i += kThreads) {
+            const uint32_t lo = i / (2 * wdt) * (2 * wdt), mid = min(lo + wdt, n), hi = min(lo + 2 * wdt, n);
+            const uint64_t key = src[i];
+            const uint32_t pos = i < mid ? (i - lo) + lower_bound64(src + mid, hi - mid, key)
+                                         : (i - mid) + lower_bound64(src + lo, mid - lo, key);
+            dst[lo + pos] = key;
+        }
+        sync_all();
+        uint64_t *tmp = src;
+        src = dst;
+        dst = tmp;
+    }
+    return src;
+}
+
+// One fast march (icvCalcFMM / icvTeleaInpaintFMM's heap order) over the
+// pixels whose stamp is INF, starting from the band in log[0, nb).  Leaves
+// every push's stamp, distance and log entry; returns the number of log
+// entries (band + pushes).
+__device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L, uint32_t &nbuckets) {
+    const int tid = threadIdx.x, ew = m.ew;
+    const int64_t off[4] = {-int64_t(ew), -1, int64_t(ew), 1};  // cv2's q = 0..3: up, left, down, right
+    uint32_t seq = nb;
+    uint32_t start[4] = {nb, nb, nb, nb};  // first push of buckets k-3 .. k (ring indexed by k & 3)
+    nbuckets = 0;
+    for (uint32_t k = 0;; ++k) {
+        uint32_t lo, hi = seq;
+        if (k == 0) {
+            lo = 0;
+            hi = nb;
+            if (nb == 0) break;
+        } else {
+            lo = k >= 3 ? start[(k - 3) & 3] : nb;
+            if (lo == seq) break;  // nothing pending in buckets >= k
+        }
+        if (k > 4u * uint32_t(m.en) + 16u) {  // cannot happen: bucket k holds T >= k/2 and T < en
+            if (tid == 0) m.meta[5] = 1u;
+            break;
+        }
+        start[k & 3] = seq;
+        // gather bucket k in push order
+        if (tid == 0) {
+            L.tmin = INF;
+            L.tmax = 0u;
+        }
+        __syncthreads();
+        uint32_t n = 0, tmn = INF, tmx = 0u;
+        for (uint32_t b = lo; b < hi; b += kThreads) {
+            const uint32_t i = b + tid;
+            float T = 0.f;
+            bool sel = false;
+            if (i < hi) {
+                T = m.logt[i];
+                sel = bucket_of(T) == k;
+            }
+            uint32_t tot;
+            const uint32_t pos = block_scan(sel ? 1u : 0u, tot, L.scr);
+            if (sel) {
+                const uint32_t tb = __float_as_uint(T + 0.0f);  // -0 -> +0: the heap compares values
+                const uint64_t key = (uint64_t(tb) << 32) | i;
+                const uint32_t at = n + pos;
+                if (at < kCap)
+                    L.keys[at] = key;
+                else
+                    m.k0[at] = key;
+                tmn = min(tmn, tb);
+                tmx = max(tmx, tb);
+            }
+            n += tot;
+        }
+        if (n == 0) continue;
+        ++nbuckets;
+        if (tmn != INF) atomicMin(&L.tmin, tmn);
+        atomicMax(&L.tmax, tmx);
+        __syncthreads();
+        const bool uniform = L.tmin == L.tmax;  // already in (T, seq) order
+        const uint64_t *keys = L.keys;
+        if (n > kCap) {
+            for (int i = tid; i < kCap; i += kThreads) m.k0[i] = L.keys[i];
+            sync_all();
+            keys = uniform ? m.k0 : global_sort(m.k0, m.k1, n, L);
+        } else if (!uniform && n > 1) {
+            int mm = 1;
+            while (mm < int(n)) mm <<= 1;
+            for (int i = int(n) + tid; i < mm; i += kThreads) L.keys[i] = ~uint64_t(0);
+            __syncthreads();
+            lds_bitonic(L.keys, mm);
+        }
+        // pops in order: claim the INSIDE neighbours (first claimant = pusher)
+        for (uint32_t r = tid; r < n; r += kThreads) {
+            const int64_t a = m.logp[uint32_t(keys[r])];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int64_t p = a + off[q];
+                if (st[p] == INF) atomicMin(&m.own[p], r * 4u + uint32_t(q));
+            }
+        }
+        sync_all();
+        // pushes numbered in (rank, direction) order
+        uint32_t npush = 0;
+        for (uint32_t b = 0; b < n; b += kThreads) {
+            const uint32_t r = b + tid;
+            int64_t a = 0;
+            unsigned mine = 0;
+            if (r < n) {
+                a = m.logp[uint32_t(keys[r])];
+#pragma unroll
+                for (int q = 0; q < 4; ++q)  // a pixel pushed by an earlier bucket keeps a stale key
+                    if (st[a + off[q]] == INF && m.own[a + off[q]] == r * 4u + uint32_t(q)) mine |= 1u << q;
+            }
+            uint32_t tot;
+            uint32_t pos = block_scan(__popc(mine), tot, L.scr);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (mine & (1u << q)) {
+                    const uint32_t s = seq + npush + pos++;
+                    const int64_t p = a + off[q];
+                    st[p] = s;
+                    m.logp[s] = uint32_t(p);
+                }
+            npush += tot;
+        }
+        sync_all();
+        // distances: sweep to the fixed point (acyclic in push order: at most
+        // npush + 1 sweeps; the cap only guards against a broken invariant)
+        for (uint32_t it = 0;; ++it) {
+            if (it > npush + 1) {
+                if (tid == 0) m.meta[5] = 2u;
+                break;
+            }
+            if (tid == 0) L.chg = 0u;
+            __syncthreads();
+            for (uint32_t i = tid; i < npush; i += kThreads) {
+                const uint32_t s = seq + i;
+                const int64_t p = m.logp[s];
+                const float T = fm_dist_seq(st, m.t, p, ew, s);
+                if (T != m.t[p]) {
+                    m.t[p] = T;
+                    L.chg = 1u;
+                }
+            }
+            sync_all();
+            const uint32_t c = L.chg;
+            __syncthreads();
+            if (!c) break;
+        }
+        for (uint32_t i = tid; i < npush; i += kThreads) m.logt[seq + i] = m.t[m.logp[seq + i]];
+        seq += npush;
+        sync_all();
+    }
+    return seq;
+}
+
+__global__ __launch_bounds__(kThreads) void sq_fmm_kernel(SqWs w) {
+    __shared__ FmmLds L;
+    const Img m = image(w, blockIdx.x);
+    const uint32_t nb = m.meta[0];
+    uint32_t nbo = 0, nbi = 0;
+    // outer march over the ring (icvCalcFMM(out, t, Out, negate = true))
+    const uint32_t no = fmm_pass(m, m.sO, nb, L, nbo);
+    for (uint32_t i = threadIdx.x; i < no; i += kThreads) {
+        const uint32_t p = m.logp[i];
+        m.t[p] = -m.t[p];
+    }
+    sync_all();
+    // inner march over the holes (icvTeleaInpaintFMM's order)
+    const uint32_t ni = fmm_pass(m, m.sI, nb, L, nbi);
+    if (threadIdx.x == 0) {
+        m.meta[1] = ni - nb;
+        m.meta[2] = 0u;
+        m.meta[4] = nbo + nbi;
+    }
+}
+
+// ---------------------------------------------------------------- COUNT / COLOUR
+// Window of a hole's colour: disk positions (a^2 + b^2 <= r^2) and their 3x3
+// neighbours (gradients, cv2's border shifts) -- symmetric, so "q is in p's
+// window" and "p is in q's window" coincide.
+__device__ __forceinline__ bool in_window(int a, int b, int r) {
+    const int a1 = max(abs(a) - 1, 0), b1 = max(abs(b) - 1, 0);
+    return a1 * a1 + b1 * b1 <= r * r;
+}
+
+// pending[p] = holes of smaller stamp in p's window; level 0 = none
+__global__ __launch_bounds__(256) void sq_count_kernel(SqWs w, int range) {
+    const int j = blockIdx.x * 64 + (threadIdx.x & 63), i = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const Img m = image(w, blockIdx.z);
+    if (i < 1 || j < 1 || i >= m.eh - 1 || j >= m.ew - 1) return;
+    const int64_t p = int64_t(i) * m.ew + j;
+    const uint32_t s = m.sI[p];
+    if (s == 0u || s == INF) return;
+    const int R = range + 1;
+    uint32_t cnt = 0;
+    for (int a = -R; a <= R; ++a) {
+        const int y = i + a;
+        if (y < 1 || y >= m.eh - 1) continue;
+        for (int b = -R; b <= R; ++b) {
+            const int x = j + b;
+            if (x < 1 || x >= m.ew - 1 || !(a || b) || !in_window(a, b, range)) continue;
+            const uint32_t sq = m.sI[int64_t(y) * m.ew + x];
+            cnt += (sq != 0u && sq < s) ? 1u : 0u;
+        }
+    }
+    m.own[p] = cnt;
+    if (cnt == 0u) {
+        uint32_t *front = reinterpret_cast<uint32_t *>(m.k0);
+        front[atomicAdd(&m.meta[2], 1u)] = uint32_t(p);
+    }
+}
+
+// cv2's Telea colour of padded hole (i, j) with stamp s, channel c (the
+// oracle's telea_colour with INSIDE = "stamp >= s"): every value it reads is
+// a pixel of smaller stamp (final) or a known pixel, or -- through cv2's
+// border index shifts -- a later hole that still holds its input value.
+__device__ __forceinline__ unsigned telea_colour_seq(const Img &m, const float *plane, int H, int W, int i, int j,
+                                                     uint32_t s, int range) {
+    const int eh = m.eh, ew = m.ew;
+    const uint32_t *st = m.sI;
+    const float *t = m.t;
+    auto IN = [&](int a, int b) -> bool { return st[int64_t(a) * ew + b] >= s; };
+    auto TT = [&](int a, int b) -> float { return t[int64_t(a) * ew + b]; };
+    auto smp = [&](int y, int x) -> int { return int(plane[int64_t(y) * W + x]); };
+    float gtx, gty;
+    const float tij = TT(i, j);
+    if (!IN(i, j + 1))
+        gtx = !IN(i, j - 1) ? (TT(i, j + 1) - TT(i, j - 1)) * 0.5f : (TT(i, j + 1) - tij);
+    else
+        gtx = !IN(i, j - 1) ? (tij - TT(i, j - 1)) : 0.f;
+    if (!IN(i + 1, j))
+        gty = !IN(i - 1, j) ? (TT(i + 1, j) - TT(i - 1, j)) * 0.5f : (TT(i + 1, j) - tij);
+    else
+        gty = !IN(i - 1, j) ? (tij - TT(i - 1, j)) : 0.f;
+    float Ia = 0, Jx = 0, Jy = 0, sum = 1.0e-20f;
+    for (int k = i - range; k <= i + range; ++k) {
+        const int km = k - 1 + (k == 1), kp = k - 1 - (k == eh - 2);
+        for (int l = j - range; l <= j + range; ++l) {
+            const int lm = l - 1 + (l == 1), lp = l - 1 - (l == ew - 2);
+            if (!(k > 0 && l > 0 && k < eh - 1 && l < ew - 1)) continue;
+            if (IN(k, l) || (l - j) * (l - j) + (k - i) * (k - i) > range * range) continue;
+            const float ry = float(i - k), rx = float(j - l);
+            const float len2 = rx * rx + ry * ry;
+            const float dst = float(1. / (double(len2) * sqrt(double(len2))));
+            const float lev = float(1. / (1 + fabs(double(TT(k, l) - tij))));
+            float dir = rx * gtx + ry * gty;
+            if (fabs(double(dir)) <= 0.01) dir = 0.000001f;
+            const float wgt = float(fabs(double(dst * lev * dir)));
+            float gix, giy;
+            if (!IN(k, l + 1))
+                gix = !IN(k, l - 1) ? float(smp(km, lp + 1) - smp(km, lm - 1)) * 2.0f : float(smp(km, lp + 1) - smp(km, lm));
+            else
+                gix = !IN(k, l - 1) ? float(smp(km, lp) - smp(km, lm - 1)) : 0.f;
+            if (!IN(k + 1, l))
+                giy = !IN(k - 1, l) ? float(smp(kp + 1, lm) - smp(km - 1, lm)) * 2.0f : float(smp(kp + 1, lm) - smp(km, lm));
+            else
+                giy = !IN(k - 1, l) ? float(smp(kp, lm) - smp(km - 1, lm)) : 0.f;
+            Ia += wgt * float(smp(km, lm));
+            Jx -= wgt * (gix * rx);
+            Jy -= wgt * (giy * ry);
+            sum += wgt;
+        }
+    }
+    (void)H;
+    const float sat = float(double(Ia / sum) + double(Jx + Jy) / (sqrt(double(Jx * Jx + Jy * Jy)) + double(1.0e-20f)) +
+                            double(0.5f));
+    return sat_u8(sat);
+}
+
+__global__ __launch_bounds__(kThreads) void sq_colour_kernel(SqWs w, float *__restrict__ out, int C, int H, int W,
+                                                             int64_t b0, int range) {
+    __shared__ uint32_t nnext;
+    const int tid = threadIdx.x;
+    const Img m = image(w, blockIdx.x);
+    const int64_t HW = int64_t(H) * W;
+    float *ob = out + (b0 + blockIdx.x) * int64_t(C) * HW;
+    uint32_t *fa = reinterpret_cast<uint32_t *>(m.k0), *fb = fa + m.en;
+    uint32_t n = m.meta[2], levels = 0;
+    const int R = range + 1;
+    if (tid == 0) nnext = 0u;
+    __syncthreads();
+    while (n) {
+        ++levels;
+        for (uint32_t e = tid; e < n; e += kThreads) {
+            const int64_t p = fa[e];
+            const int i = int(p / m.ew), j = int(p - int64_t(i) * m.ew);
+            const uint32_t s = m.sI[p];
+            for (int c = 0; c < C; ++c) {
+                float *pl = ob + c * HW;
+                pl[int64_t(i - 1) * W + (j - 1)] = float(telea_colour_seq(m, pl, H, W, i, j, s, range));
+            }
+            // release the holes of larger stamp that read this one
+            for (int a = -R; a <= R; ++a) {
+                const int y = i + a;
+                if (y < 1 || y >= m.eh - 1) continue;
+                for (int b = -R; b <= R; ++b) {
+                    const int x = j + b;
+                    if (x < 1 || x >= m.ew - 1 || !(a || b) || !in_window(a, b, range)) continue;
+                    const int64_t q = int64_t(y) * m.ew + x;
+                    const uint32_t sq = m.sI[q];
+                    if (sq > s && sq != INF && atomicSub(&m.own[q], 1u) == 1u) fb[atomicAdd(&nnext, 1u)] = uint32_t(q);
+                }
+            }
+        }
+        sync_all();
+        n = nnext;
+        __syncthreads();
+        if (tid == 0) nnext = 0u;
+        uint32_t *tmp = fa;
+        fa = fb;
+        fb = tmp;
+        __syncthreads();
+    }
+    if (tid == 0) m.meta[3] = levels;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t ofd_inpaint_seq_workspace_bytes(int64_t B, int64_t H, int64_t W) {
+    if (B <= 0 || H <= 0 || W <= 0) return 0;
+    return size_t(B) * per_image_bytes(H, W) + 8 * 256;
+}
+
+int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float *collision, float *out, int64_t B,
+                              int64_t C, int64_t H, int64_t W, int radius, void *workspace, size_t workspace_bytes,
+                              void *stream) {
+    if (B < 0 || C < 0 || H < 0 || W < 0) return OFD_FW_EINVAL;
+    if (B * C * H * W == 0) return OFD_FW_OK;
+    if (!img || !valid || !collision || !out) return OFD_FW_EINVAL;
+    if (H < 2 || W < 2) return OFD_FW_EINVAL;
+    const int64_t en = (H + 2) * (W + 2);
+    if (en >= (int64_t(1) << 30)) return OFD_FW_ETOOBIG;  // ranks * 4 + direction fit 32 bits
+    const int r = radius < 1 ? 1 : (radius > kMaxRange ? kMaxRange : radius);
+    if (!workspace || (reinterpret_cast<uintptr_t>(workspace) & 255u)) return OFD_FW_EWORKSPACE;
+    const size_t pi = per_image_bytes(H, W), fixed = 8 * 256;
+    if (workspace_bytes < fixed + pi) return OFD_FW_EWORKSPACE;
+    int64_t G = int64_t((workspace_bytes - fixed) / pi);
+    if (G > B) G = B;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const SqWs w = carve(workspace, G, H, W);
+    for (int64_t b0 = 0; b0 < B; b0 += G) {
+        const int64_t nb = B - b0 < G ? B - b0 : G;
+        hipLaunchKernelGGL(sq_prep_kernel, dim3(unsigned((W + 63) / 64), unsigned((H + 3) / 4), unsigned(nb)), dim3(256),
+                           0, st, img, valid, collision, out, w, int(C), int(H), int(W), b0);
+        hipLaunchKernelGGL(sq_init_kernel, dim3(unsigned((w.eh + 3) / 4), unsigned(nb)), dim3(256), 0, st, w, r);
+        hipLaunchKernelGGL(sq_band_scan_kernel, dim3(unsigned(nb)), dim3(kThreads), 0, st, w);
+        hipLaunchKernelGGL(sq_band_write_kernel, dim3(unsigned((w.eh + 3) / 4), unsigned(nb)), dim3(256), 0, st, w);
+        hipLaunchKernelGGL(sq_fmm_kernel, dim3(unsigned(nb)), dim3(kThreads), 0, st, w);
+        hipLaunchKernelGGL(sq_count_kernel, dim3(unsigned((w.ew + 63) / 64), unsigned((w.eh + 3) / 4), unsigned(nb)),
+                           dim3(256), 0, st, w, r);
+        hipLaunchKernelGGL(sq_colour_kernel, dim3(unsigned(nb)), dim3(kThreads), 0, st, w, out, int(C), int(H), int(W),
+                           b0, r);
+    }
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? OFD_FW_OK : int(e);
+}
+
+}  // extern "C"

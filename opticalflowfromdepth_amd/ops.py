@@ -21,6 +21,7 @@ There is no CPU path: the reference raises for non-GPU tensors
 """
 from __future__ import annotations
 
+import os
 import threading
 from collections import OrderedDict
 from typing import List, Tuple
@@ -191,23 +192,44 @@ def forward_warp_flow(obj: torch.Tensor, flow: torch.Tensor, depth: torch.Tensor
     return output, valid, collision
 
 
-def inpaint(img: torch.Tensor, valid: torch.Tensor, collision: torch.Tensor, radius: int = 3) -> torch.Tensor:
+INPAINT_ORDERS = ("sequential", "layered")
+
+
+def default_inpaint_order() -> str:
+    """The hole-fill order ops.inpaint uses when none is given: OFD_INPAINT_ORDER, else "sequential"."""
+    o = os.environ.get("OFD_INPAINT_ORDER", "sequential")
+    if o not in INPAINT_ORDERS:
+        raise ValueError(f"OFD_INPAINT_ORDER must be one of {INPAINT_ORDERS}, got {o!r}")
+    return o
+
+
+def inpaint(img: torch.Tensor, valid: torch.Tensor, collision: torch.Tensor, radius: int = 3,
+            order: str = None) -> torch.Tensor:
     """Drop-in for ``utils.inpaint(img, valid, collision)`` (utils.py:136-151), batched.
 
     img [C,H,W] with valid / collision [1,H,W] (the reference's call shape), or
     img [B,C,H,W] with [B,1,H,W] masks.  Pixels the keep mask of
-    utils.py:137-142 drops are filled (Telea weights, layered marching; see
+    utils.py:137-142 drops are filled (Telea; see
     include/ofd_inpaint.h); every pixel of the result is float32 of the
     uint8 cast of utils.py:148, on img's device, like the reference's return.
 
-    The fill values are NOT cv2's: holes are finalised in layers of equal L1
-    distance instead of cv2's one-at-a-time heap order.  The specified
-    divergence (tests/test_inpaint.py): on warped
-    random-RGB images 85 % of hole values differ from the sequential order,
-    mean 5.7 grey levels, p99 40; within 1-2 levels on smooth images.  Kept
-    pixels, the mask algebra and the cast are the reference's exactly.  The
-    call never blocks the host.
+    ``order="sequential"`` (the default, include/ofd_inpaint.h
+    ofd_inpaint_telea_seq_f32) fills in cv2's exact order: heap pops by
+    (distance, push order), each hole coloured from the pixels reached before
+    it -- bit-exact against the CPU restatement of OpenCV's Telea
+    (oracle/inpaint_oracle.c; OpenCV itself is absent from the build image).
+    ``order="layered"`` (ofd_inpaint_telea_f32) is the faster re-specification:
+    holes are finalised in layers of equal L1 distance, so its values are NOT
+    cv2's -- the specified divergence (DESIGN.md section 5,
+    tests/test_inpaint.py): on warped random-RGB images 85 % of hole values
+    differ from the sequential order, mean 5.7 grey levels, p99 40; within 1-2
+    levels on smooth images.  Both keep the reference's mask algebra, cast and
+    kept pixels exactly.  The call never blocks the host.
     """
+    order = default_inpaint_order() if order is None else order
+    if order not in INPAINT_ORDERS:
+        raise ValueError(f"order must be one of {INPAINT_ORDERS}, got {order!r}")
+    seq = order == "sequential"
     for x, n in ((img, "img"), (valid, "valid"), (collision, "collision")):
         if not isinstance(x, torch.Tensor):
             raise TypeError(f"{n} must be a torch.Tensor")
@@ -233,7 +255,7 @@ def inpaint(img: torch.Tensor, valid: torch.Tensor, collision: torch.Tensor, rad
         collision = collision.to(_F32).contiguous()
         out = torch.empty_like(img)
         lib = _native.lib()
-        nbytes = int(lib.ofd_inpaint_workspace_bytes(B, H, W))
+        nbytes = int((lib.ofd_inpaint_seq_workspace_bytes if seq else lib.ofd_inpaint_workspace_bytes)(B, H, W))
         ws = None
         if nbytes:
             key = (dev.index, stream.cuda_stream)
@@ -245,10 +267,10 @@ def inpaint(img: torch.Tensor, valid: torch.Tensor, collision: torch.Tensor, rad
                     with torch.cuda.stream(stream):
                         ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
                 _cache_put(_ip_workspaces, key, ws)
-        rc = lib.ofd_inpaint_telea_f32(img.data_ptr(), valid.data_ptr(), collision.data_ptr(), out.data_ptr(),
-                                       B, C, H, W, int(radius),
-                                       ws.data_ptr() if ws is not None else None,
-                                       ws.numel() if ws is not None else 0, stream.cuda_stream)
+        fn = lib.ofd_inpaint_telea_seq_f32 if seq else lib.ofd_inpaint_telea_f32
+        rc = fn(img.data_ptr(), valid.data_ptr(), collision.data_ptr(), out.data_ptr(),
+                B, C, H, W, int(radius), ws.data_ptr() if ws is not None else None,
+                ws.numel() if ws is not None else 0, stream.cuda_stream)
         _native.check(rc, "inpaint")
     return out[0] if squeeze else out
 

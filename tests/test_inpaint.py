@@ -147,10 +147,79 @@ def test_inpaint_gpu_bit_exact_vs_layered_oracle(case):
     name, img, v, c, r = case
     dev = torch.device("cuda:0")
     got = ops.inpaint(torch.from_numpy(img).to(dev), torch.from_numpy(v).to(dev), torch.from_numpy(c).to(dev),
-                      radius=r).cpu().numpy()
+                      radius=r, order="layered").cpu().numpy()
     exp = oracle.inpaint(img, v, c, r, layered=True)
     bad = np.argwhere(got != exp)
     assert bad.size == 0, f"{name}: {len(bad)} differing values, first {bad[:5].tolist()}"
+
+
+def _seq_extra_cases():
+    """Shapes that stress the bucketed march: curved and diagonal fronts (many
+    distinct distances per bucket), buckets above the LDS sort capacity with
+    distinct distances (scattered holes over a large image), a hole touching
+    every border, thin snakes (long distance chains), a one-pixel frame of
+    known pixels."""
+    rng = np.random.default_rng(11)
+    cases = []
+    h, w = 96, 120
+    yy, xx = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
+    img = smooth_image(h, w, 3)[None]
+    v = np.ones((1, 1, h, w), np.float32)
+    v[0, 0][(yy - 40) ** 2 + (xx - 60) ** 2 < 30 ** 2] = 0
+    v[0, 0][np.abs(yy - xx) < 4] = 0
+    cases.append(("disk_diag", img * v, v, np.zeros_like(v), 3))
+    h, w = 200, 300  # band ~ 20 k pixels, distances 0.707 / 0.966 / 1 ... per bucket
+    img = rng.integers(0, 256, (1, 3, h, w)).astype(np.float32)
+    v = (rng.random((1, 1, h, w)) < 0.55).astype(np.float32)
+    cases.append(("scattered200x300", img, v, np.zeros_like(v), 3))
+    h, w = 64, 80
+    img = smooth_image(h, w, 4)[None]
+    v = np.zeros((1, 1, h, w), np.float32)
+    v[..., 20:44, 30:50] = 1  # a known island: the hole touches every border
+    cases.append(("island", img * v, v, np.zeros_like(v), 3))
+    v = np.ones((1, 1, h, w), np.float32)
+    for k in range(4, h - 4, 6):  # snake: long thin corridors
+        v[..., k:k + 2, 2:w - 2] = 0
+        v[..., k:k + 6, (2 if (k // 6) % 2 else w - 4):(4 if (k // 6) % 2 else w - 2)] = 0
+    cases.append(("snake", img * v, v, np.zeros_like(v), 3))
+    v = np.zeros((1, 1, h, w), np.float32)
+    v[..., 0, :] = v[..., -1, :] = v[..., :, 0] = v[..., :, -1] = 1
+    cases.append(("frame_only", img * v, v, np.zeros_like(v), 3))
+    img = rng.integers(0, 256, (2, 3, 48, 64)).astype(np.float32)
+    v = np.ones((2, 1, 48, 64), np.float32)
+    v[0, :, :, :25] = 0   # left border band (ego-motion strip)
+    v[1, :, 30:, :] = 0   # bottom band
+    cases.append(("border_bands", img * v, v, np.zeros_like(v), 3))
+    return cases
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", _gpu_cases() + _seq_extra_cases(), ids=lambda c: c[0])
+def test_inpaint_gpu_bit_exact_vs_sequential_oracle(case):
+    """order="sequential": cv2's heap order (the oracle's restatement of
+    icvCalcFMM / icvTeleaInpaintFMM), bit for bit."""
+    from opticalflowfromdepth_amd import ops
+    name, img, v, c, r = case
+    dev = torch.device("cuda:0")
+    got = ops.inpaint(torch.from_numpy(img).to(dev), torch.from_numpy(v).to(dev), torch.from_numpy(c).to(dev),
+                      radius=r, order="sequential").cpu().numpy()
+    exp = oracle.inpaint(img, v, c, r, layered=False)
+    bad = np.argwhere(got != exp)
+    assert bad.size == 0, f"{name}: {len(bad)} differing values, first {bad[:5].tolist()}"
+
+
+@pytest.mark.gpu
+def test_inpaint_sequential_after_warp_headline_shape():
+    """The pipeline's use at the headline shape: FW then inpaint the warped RGB
+    (preprocess.py:358-366), 768x1024, disparity and ego-motion holes, cv2 order."""
+    from opticalflowfromdepth_amd import forward_warp_flow, ops, synth
+    dev = torch.device("cuda:0")
+    obj, flow, depth = synth.stage_one_batch([12345, 12346, 12377, 12378], 768, 1024, dev)
+    out, valid, coll = forward_warp_flow(obj, flow, depth)
+    rgb = (out[:, 0:3] * valid).contiguous()
+    got = ops.inpaint(rgb, valid, coll, order="sequential").cpu().numpy()
+    exp = oracle.inpaint(rgb.cpu().numpy(), valid.cpu().numpy(), coll.cpu().numpy(), 3, layered=False)
+    assert np.array_equal(got, exp)
 
 
 @pytest.mark.gpu
@@ -174,7 +243,7 @@ def test_inpaint_after_warp_headline_shape():
     obj, flow, depth = synth.stage_one_batch(seeds, 768, 1024, dev)
     out, valid, coll = forward_warp_flow(obj, flow, depth)
     rgb = (out[:, 0:3] * valid).contiguous()
-    got = ops.inpaint(rgb, valid, coll).cpu().numpy()
+    got = ops.inpaint(rgb, valid, coll, order="layered").cpu().numpy()
     exp = oracle.inpaint(rgb.cpu().numpy(), valid.cpu().numpy(), coll.cpu().numpy(), 3, layered=True)
     assert np.array_equal(got, exp)
 
@@ -199,7 +268,7 @@ def test_inpaint_gpu_schedules_bit_exact(sched):
             exp = oracle.inpaint(img, v, c, r, layered=True)
             for rep in range(2):  # the second call sees the first one's layer statistics
                 got = ops.inpaint(torch.from_numpy(img).to(dev), torch.from_numpy(v).to(dev),
-                                  torch.from_numpy(c).to(dev), radius=r)
+                                  torch.from_numpy(c).to(dev), radius=r, order="layered")
                 torch.cuda.synchronize()
                 bad = np.argwhere(got.cpu().numpy() != exp)
                 assert bad.size == 0, f"{name} {sched} rep{rep}: {len(bad)} differing, first {bad[:5].tolist()}"
