@@ -61,11 +61,28 @@ namespace {
 
 #include "ip_common.h"
 
+// Probe build only (-DOFD_SQ_PROF, tools/seq_probe.sh): thread 0 of each
+// workgroup accumulates shader-clock intervals of its own work into meta[8..].
+#ifdef OFD_SQ_PROF
+__device__ __forceinline__ uint64_t sq_clock() {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    return __builtin_amdgcn_s_memtime();
+}
+#define SQ_T(var) uint64_t var = (threadIdx.x == 0) ? sq_clock() : 0
+#define SQ_ACC(slot, a, b) do { if (threadIdx.x == 0) prof[slot] += (b) - (a); } while (0)
+#else
+#define SQ_T(var) do { } while (0)
+#define SQ_ACC(slot, a, b) do { } while (0)
+#endif
+
 constexpr uint32_t INF = 0xFFFFFFFFu;
-constexpr int kThreads = 1024;  // FMM / COLOUR workgroup
+constexpr int kThreads = 1024;     // FMM workgroup
+constexpr int kColThreads = 256;  // COLOUR workgroup of the any-radius path
 constexpr int kCap = 4096;      // bucket keys sorted in LDS; larger buckets merge in global memory
+constexpr int kLdsPush = 2048;  // pushes per bucket whose distance sweeps run in LDS
 constexpr int kMaxRange = 100;
-constexpr int kMeta = 8;  // per image: 0 band count, 1 pushes, 2 frontier count, 3 levels, 4 buckets, 5 error
+constexpr int kMeta = 32;  // per image: 0 band count, 1 pushes, 2 frontier count, 3 levels, 4 buckets, 5 error,
+                          // 8..15 FMM / 16..23 COLOUR probe clocks (>> 8)
 
 inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
@@ -86,7 +103,7 @@ struct SqWs {
 
 size_t per_image_bytes(int64_t H, int64_t W) {
     const size_t en = size_t(H + 2) * size_t(W + 2);
-    return align256(en * 4) * 6 + align256(en * 8) * 2 + align256(size_t(H + 2) * 4) + 256;
+    return align256(en * 4) * 6 + align256(en * 8) * 2 + align256(size_t(H + 2) * 4) + kMeta * 4;
 }
 
 SqWs carve(void *ws, int64_t G, int64_t H, int64_t W) {
@@ -369,7 +386,8 @@ __device__ uint64_t *global_sort(uint64_t *g, uint64_t *h, uint32_t n, FmmLds &L
 // pixels whose stamp is INF, starting from the band in log[0, nb).  Leaves
 // every push's stamp, distance and log entry; returns the number of log
 // entries (band + pushes).
-__device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L, uint32_t &nbuckets) {
+__device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L, uint32_t &nbuckets, uint64_t *prof) {
+    (void)prof;
     const int tid = threadIdx.x, ew = m.ew;
     const int64_t off[4] = {-int64_t(ew), -1, int64_t(ew), 1};  // cv2's q = 0..3: up, left, down, right
     uint32_t seq = nb;
@@ -390,6 +408,7 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
             break;
         }
         start[k & 3] = seq;
+        SQ_T(f0);
         // gather bucket k in push order
         if (tid == 0) {
             L.tmin = INF;
@@ -420,6 +439,8 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
             }
             n += tot;
         }
+        SQ_T(f1);
+        SQ_ACC(0, f0, f1);
         if (n == 0) continue;
         ++nbuckets;
         if (tmn != INF) atomicMin(&L.tmin, tmn);
@@ -432,12 +453,27 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
             sync_all();
             keys = uniform ? m.k0 : global_sort(m.k0, m.k1, n, L);
         } else if (!uniform && n > 1) {
-            int mm = 1;
-            while (mm < int(n)) mm <<= 1;
-            for (int i = int(n) + tid; i < mm; i += kThreads) L.keys[i] = ~uint64_t(0);
-            __syncthreads();
-            lds_bitonic(L.keys, mm);
+            if (n <= 512) {
+                // rank sort (unique keys): each key's place is the number of
+                // smaller keys -- broadcast LDS reads, no barrier per stage
+                for (uint32_t i = tid; i < n; i += kThreads) {
+                    const uint64_t key = L.keys[i];
+                    uint32_t r = 0;
+                    for (uint32_t j2 = 0; j2 < n; ++j2) r += L.keys[j2] < key ? 1u : 0u;
+                    L.keys[kCap / 2 + r] = key;
+                }
+                __syncthreads();
+                keys = L.keys + kCap / 2;
+            } else {
+                int mm = 1;
+                while (mm < int(n)) mm <<= 1;
+                for (int i = int(n) + tid; i < mm; i += kThreads) L.keys[i] = ~uint64_t(0);
+                __syncthreads();
+                lds_bitonic(L.keys, mm);
+            }
         }
+        SQ_T(f2);
+        SQ_ACC(1, f1, f2);
         // pops in order: claim the INSIDE neighbours (first claimant = pusher)
         for (uint32_t r = tid; r < n; r += kThreads) {
             const int64_t a = m.logp[uint32_t(keys[r])];
@@ -448,6 +484,8 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
             }
         }
         sync_all();
+        SQ_T(f3);
+        SQ_ACC(2, f2, f3);
         // pushes numbered in (rank, direction) order
         uint32_t npush = 0;
         for (uint32_t b = 0; b < n; b += kThreads) {
@@ -473,8 +511,82 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
             npush += tot;
         }
         sync_all();
+        SQ_T(f4);
+        SQ_ACC(3, f3, f4);
         // distances: sweep to the fixed point (acyclic in push order: at most
-        // npush + 1 sweeps; the cap only guards against a broken invariant)
+        // npush + 1 sweeps; the cap only guards against a broken invariant).
+        // Up to kLdsPush pushes: the bucket's distances live in LDS and each
+        // push keeps its neighbours' fixed values in registers -- only a
+        // neighbour pushed earlier in this bucket is read per sweep.
+        if (npush <= uint32_t(kLdsPush)) {
+            float *Tl = reinterpret_cast<float *>(L.keys);
+            float fv[2][4];
+            int lk[2][4];  // -2: INSIDE, -1: fixed value, >= 0: push index in this bucket
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const uint32_t i = tid + uint32_t(u) * kThreads;
+                if (i < npush) {
+                    const uint32_t sp = seq + i;
+                    const int64_t p = m.logp[sp];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int64_t nq = p + off[q];
+                        const uint32_t sn = st[nq];
+                        lk[u][q] = sn >= sp ? -2 : (sn >= seq ? int(sn - seq) : -1);
+                        fv[u][q] = lk[u][q] == -1 ? m.t[nq] : T_FAR;
+                    }
+                    Tl[i] = T_FAR;
+                }
+            }
+            __syncthreads();
+            for (uint32_t it = 0;; ++it) {
+                if (it > npush + 1) {
+                    if (tid == 0) m.meta[5] = 2u;
+                    break;
+                }
+                if (tid == 0) L.chg = 0u;
+                __syncthreads();
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const uint32_t i = tid + uint32_t(u) * kThreads;
+                    if (i < npush) {
+                        float tv[4];
+                        bool in[4];
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            in[q] = lk[u][q] == -2;
+                            tv[q] = lk[u][q] >= 0 ? Tl[lk[u][q]] : fv[u][q];
+                        }
+                        // cv2's order: (up, left), (down, left), (up, right), (down, right)
+                        const float T = min4f(fm_solve(tv[0], in[0], tv[1], in[1]), fm_solve(tv[2], in[2], tv[1], in[1]),
+                                              fm_solve(tv[0], in[0], tv[3], in[3]), fm_solve(tv[2], in[2], tv[3], in[3]));
+                        if (T != Tl[i]) {
+                            Tl[i] = T;
+                            L.chg = 1u;
+                        }
+                    }
+                }
+                __syncthreads();
+                const uint32_t c = L.chg;
+                __syncthreads();
+#ifdef OFD_SQ_PROF
+                if (tid == 0) prof[6] += 1;
+#endif
+                if (!c) break;
+            }
+            for (uint32_t i = tid; i < npush; i += kThreads) {
+                const float T = Tl[i];
+                m.t[m.logp[seq + i]] = T;
+                m.logt[seq + i] = T;
+            }
+            SQ_T(f5a);
+            SQ_ACC(4, f4, f5a);
+            seq += npush;
+            sync_all();
+            SQ_T(f6a);
+            SQ_ACC(5, f5a, f6a);
+            continue;
+        }
         for (uint32_t it = 0;; ++it) {
             if (it > npush + 1) {
                 if (tid == 0) m.meta[5] = 2u;
@@ -494,11 +606,18 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
             sync_all();
             const uint32_t c = L.chg;
             __syncthreads();
+#ifdef OFD_SQ_PROF
+            if (tid == 0) prof[6] += 1;
+#endif
             if (!c) break;
         }
+        SQ_T(f5);
+        SQ_ACC(4, f4, f5);
         for (uint32_t i = tid; i < npush; i += kThreads) m.logt[seq + i] = m.t[m.logp[seq + i]];
         seq += npush;
         sync_all();
+        SQ_T(f6);
+        SQ_ACC(5, f5, f6);
     }
     return seq;
 }
@@ -509,18 +628,20 @@ __global__ __launch_bounds__(kThreads) void sq_fmm_kernel(SqWs w) {
     const uint32_t nb = m.meta[0];
     uint32_t nbo = 0, nbi = 0;
     // outer march over the ring (icvCalcFMM(out, t, Out, negate = true))
-    const uint32_t no = fmm_pass(m, m.sO, nb, L, nbo);
+    uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const uint32_t no = fmm_pass(m, m.sO, nb, L, nbo, prof);
     for (uint32_t i = threadIdx.x; i < no; i += kThreads) {
         const uint32_t p = m.logp[i];
         m.t[p] = -m.t[p];
     }
     sync_all();
     // inner march over the holes (icvTeleaInpaintFMM's order)
-    const uint32_t ni = fmm_pass(m, m.sI, nb, L, nbi);
+    const uint32_t ni = fmm_pass(m, m.sI, nb, L, nbi, prof);
     if (threadIdx.x == 0) {
         m.meta[1] = ni - nb;
         m.meta[2] = 0u;
         m.meta[4] = nbo + nbi;
+        for (int k = 0; k < 8; ++k) m.meta[8 + k] = uint32_t(k == 6 ? prof[k] : prof[k] >> 8);
     }
 }
 
@@ -531,6 +652,14 @@ __global__ __launch_bounds__(kThreads) void sq_fmm_kernel(SqWs w) {
 __device__ __forceinline__ bool in_window(int a, int b, int r) {
     const int a1 = max(abs(a) - 1, 0), b1 = max(abs(b) - 1, 0);
     return a1 * a1 + b1 * b1 <= r * r;
+}
+
+// Radius-3 window positions (patch offsets a, b in [-4, 4]): the disk and
+// its 3x3 neighbourhood.
+constexpr bool disk3(int a, int b) { return a * a + b * b <= 9; }
+constexpr bool win3(int a, int b) {
+    const int a1 = (a < 0 ? -a : a) - 1, b1 = (b < 0 ? -b : b) - 1;
+    return (a1 < 0 ? 0 : a1) * (a1 < 0 ? 0 : a1) + (b1 < 0 ? 0 : b1) * (b1 < 0 ? 0 : b1) <= 9;
 }
 
 // pending[p] = holes of smaller stamp in p's window; level 0 = none
@@ -564,8 +693,8 @@ __global__ __launch_bounds__(256) void sq_count_kernel(SqWs w, int range) {
 // oracle's telea_colour with INSIDE = "stamp >= s"): every value it reads is
 // a pixel of smaller stamp (final) or a known pixel, or -- through cv2's
 // border index shifts -- a later hole that still holds its input value.
-__device__ __forceinline__ unsigned telea_colour_seq(const Img &m, const float *plane, int H, int W, int i, int j,
-                                                     uint32_t s, int range) {
+__device__ __forceinline__ unsigned telea_colour_seq(const Img &m, const float *plane, int W, int i, int j, uint32_t s,
+                                                     int range) {
     const int eh = m.eh, ew = m.ew;
     const uint32_t *st = m.sI;
     const float *t = m.t;
@@ -611,35 +740,40 @@ __device__ __forceinline__ unsigned telea_colour_seq(const Img &m, const float *
             sum += wgt;
         }
     }
-    (void)H;
     const float sat = float(double(Ia / sum) + double(Jx + Jy) / (sqrt(double(Jx * Jx + Jy * Jy)) + double(1.0e-20f)) +
                             double(0.5f));
     return sat_u8(sat);
 }
 
-__global__ __launch_bounds__(kThreads) void sq_colour_kernel(SqWs w, float *__restrict__ out, int C, int H, int W,
+struct ColLds {
+    uint32_t nnext;
+};
+
+// Any radius: one thread per hole, dependants released by atomic counters.
+__global__ __launch_bounds__(kColThreads) void sq_colour_kernel(SqWs w, float *__restrict__ out, int C, int H, int W,
                                                              int64_t b0, int range) {
-    __shared__ uint32_t nnext;
+    __shared__ ColLds L;
     const int tid = threadIdx.x;
     const Img m = image(w, blockIdx.x);
     const int64_t HW = int64_t(H) * W;
     float *ob = out + (b0 + blockIdx.x) * int64_t(C) * HW;
     uint32_t *fa = reinterpret_cast<uint32_t *>(m.k0), *fb = fa + m.en;
+    uint32_t *lsz = reinterpret_cast<uint32_t *>(m.k1);  // diagnostics: size of each level (tools/seq_time.py)
     uint32_t n = m.meta[2], levels = 0;
     const int R = range + 1;
-    if (tid == 0) nnext = 0u;
+    if (tid == 0) L.nnext = 0u;
     __syncthreads();
     while (n) {
+        if (tid == 0 && levels < uint32_t(2 * m.en)) lsz[levels] = n;
         ++levels;
-        for (uint32_t e = tid; e < n; e += kThreads) {
+        for (uint32_t e = tid; e < n; e += kColThreads) {
             const int64_t p = fa[e];
             const int i = int(p / m.ew), j = int(p - int64_t(i) * m.ew);
             const uint32_t s = m.sI[p];
             for (int c = 0; c < C; ++c) {
                 float *pl = ob + c * HW;
-                pl[int64_t(i - 1) * W + (j - 1)] = float(telea_colour_seq(m, pl, H, W, i, j, s, range));
+                pl[int64_t(i - 1) * W + (j - 1)] = float(telea_colour_seq(m, pl, W, i, j, s, range));
             }
-            // release the holes of larger stamp that read this one
             for (int a = -R; a <= R; ++a) {
                 const int y = i + a;
                 if (y < 1 || y >= m.eh - 1) continue;
@@ -648,20 +782,276 @@ __global__ __launch_bounds__(kThreads) void sq_colour_kernel(SqWs w, float *__re
                     if (x < 1 || x >= m.ew - 1 || !(a || b) || !in_window(a, b, range)) continue;
                     const int64_t q = int64_t(y) * m.ew + x;
                     const uint32_t sq = m.sI[q];
-                    if (sq > s && sq != INF && atomicSub(&m.own[q], 1u) == 1u) fb[atomicAdd(&nnext, 1u)] = uint32_t(q);
+                    if (sq > s && sq != INF && atomicSub(&m.own[q], 1u) == 1u) fb[atomicAdd(&L.nnext, 1u)] = uint32_t(q);
                 }
             }
         }
         sync_all();
-        n = nnext;
+        n = L.nnext;
         __syncthreads();
-        if (tid == 0) nnext = 0u;
+        if (tid == 0) L.nnext = 0u;
         uint32_t *tmp = fa;
         fa = fb;
         fb = tmp;
         __syncthreads();
     }
     if (tid == 0) m.meta[3] = levels;
+}
+
+// Radius 3 (the reference's inpaintRange): a group of 16 lanes per hole, 64
+// holes in flight per workgroup.  Lane g of a group owns disk positions g and
+// g + 16 (cv2's raster order over the 29 positions of the r = 3 disk) and
+// loads what they need -- stamps of the position and its 4-neighbours, its
+// distance, and per channel the (up to 7) values cv2's gradient reads, with
+// its border index shifts -- so the only cross-lane traffic is the ordered
+// sums: cv2 adds the window's terms in (k, l) order, and so does the group,
+// one shuffle per term.  Release: lanes own the 60 window positions 16 apart.
+constexpr int kG = 16;
+constexpr int kG16Threads = 512;  // 170 VGPRs: two waves per SIMD
+constexpr int kGroups = kG16Threads / kG;
+
+constexpr int disk_count() {
+    int n = 0;
+    for (int a = -3; a <= 3; ++a)
+        for (int b = -3; b <= 3; ++b) n += disk3(a, b) ? 1 : 0;
+    return n;
+}
+constexpr int win_count() {
+    int n = 0;
+    for (int a = -4; a <= 4; ++a)
+        for (int b = -4; b <= 4; ++b) n += (win3(a, b) && (a || b)) ? 1 : 0;
+    return n;
+}
+constexpr int kDisk = disk_count();  // 29
+constexpr int kWin = win_count();    // 60
+static_assert(kDisk <= 2 * kG && kWin <= 4 * kG, "radius-3 window does not fit the lane group");
+
+// d-th position (raster order) of the disk / of the window without its centre
+__device__ __forceinline__ void disk_pos(int d, int &a, int &b) {
+    int n = 0;
+    a = b = 0;
+    for (int u = -3; u <= 3; ++u)
+        for (int v = -3; v <= 3; ++v)
+            if (disk3(u, v)) {
+                if (n == d) {
+                    a = u;
+                    b = v;
+                }
+                ++n;
+            }
+}
+__device__ __forceinline__ void win_pos(int d, int &a, int &b) {
+    int n = 0;
+    a = b = 0;
+    for (int u = -4; u <= 4; ++u)
+        for (int v = -4; v <= 4; ++v)
+            if (win3(u, v) && (u || v)) {
+                if (n == d) {
+                    a = u;
+                    b = v;
+                }
+                ++n;
+            }
+}
+
+constexpr int kChunkC = 4;  // channels whose values are loaded together
+
+struct G16Lds {
+    uint32_t nnext;
+    float terms[kGroups][kChunkC][3][2 * kG];  // per group: Ia / Jx / Jy terms of each disk position
+    float wts[kGroups][2 * kG];                // per group: weight of each disk position
+};
+
+__global__ __launch_bounds__(kG16Threads) void sq_colour_g16_kernel(SqWs w, float *__restrict__ out, int C, int H, int W,
+                                                                   int64_t b0) {
+    __shared__ G16Lds L;
+    const int tid = threadIdx.x, g = tid / kG, gl = tid % kG;
+    const Img m = image(w, blockIdx.x);
+    const int eh = m.eh, ew = m.ew;
+    const int64_t HW = int64_t(H) * W;
+    float *ob = out + (b0 + blockIdx.x) * int64_t(C) * HW;
+    uint32_t *fa = reinterpret_cast<uint32_t *>(m.k0), *fb = fa + m.en;
+    uint32_t *lsz = reinterpret_cast<uint32_t *>(m.k1);
+    // this lane's disk positions (slot 0, 1) and window positions (release)
+    int da[2], db[2], wa[4], wb[4];
+    bool dv[2], wv[4];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        dv[k] = gl + kG * k < kDisk;
+        disk_pos(gl + kG * k, da[k], db[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        wv[k] = gl + kG * k < kWin;
+        win_pos(gl + kG * k, wa[k], wb[k]);
+    }
+    uint32_t n = m.meta[2], levels = 0;
+    if (tid == 0) L.nnext = 0u;
+    __syncthreads();
+    uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    (void)prof;
+    auto clampi = [&](int y, int x) -> int64_t {
+        return int64_t(min(max(y, 0), eh - 1)) * ew + min(max(x, 0), ew - 1);
+    };
+    while (n) {
+        if (tid == 0 && levels < uint32_t(2 * m.en)) lsz[levels] = n;
+        ++levels;
+        SQ_T(l0);
+        for (uint32_t e = g; e < n; e += kGroups) {
+            SQ_T(c0);
+            const int64_t p = fa[e];
+            const int i = int(p / ew), j = int(p - int64_t(i) * ew);
+            const uint32_t s = m.sI[p];
+            // every load of the hole up front: the gradient's neighbours, this
+            // lane's disk positions, and the window stamps for the release
+            const uint32_t su = m.sI[p - ew], sd = m.sI[p + ew], sl = m.sI[p - 1], sr = m.sI[p + 1];
+            const float tij = m.t[p], tu = m.t[p - ew], td = m.t[p + ew], tl = m.t[p - 1], tr = m.t[p + 1];
+            uint32_t sc[2], sR[2], sL[2], sD[2], sU[2];
+            float tk[2];
+            bool inimg[2];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int y = i + da[k], x = j + db[k];
+                inimg[k] = dv[k] && y > 0 && x > 0 && y < eh - 1 && x < ew - 1;
+                sc[k] = m.sI[clampi(y, x)];
+                sR[k] = m.sI[clampi(y, x + 1)];
+                sL[k] = m.sI[clampi(y, x - 1)];
+                sD[k] = m.sI[clampi(y + 1, x)];
+                sU[k] = m.sI[clampi(y - 1, x)];
+                tk[k] = m.t[clampi(y, x)];
+            }
+            uint32_t sw[4];
+            int64_t qq[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int y = i + wa[k], x = j + wb[k];
+                const bool ok = wv[k] && y > 0 && x > 0 && y < eh - 1 && x < ew - 1;
+                qq[k] = clampi(y, x);
+                sw[k] = m.sI[qq[k]];
+                sw[k] = ok ? sw[k] : 0u;
+            }
+            SQ_T(c1);
+            float gtx, gty;
+            if (!(sr >= s))
+                gtx = !(sl >= s) ? (tr - tl) * 0.5f : (tr - tij);
+            else
+                gtx = !(sl >= s) ? (tij - tl) : 0.f;
+            if (!(sd >= s))
+                gty = !(su >= s) ? (td - tu) * 0.5f : (td - tij);
+            else
+                gty = !(su >= s) ? (tij - tu) : 0.f;
+            float wt[2];
+            bool used[2];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                used[k] = inimg[k] && !(sc[k] >= s);
+                const float ry = float(-da[k]), rx = float(-db[k]);
+                const float len2 = rx * rx + ry * ry;
+                const float dst = float(1. / (double(len2) * sqrt(double(len2))));
+                const float lev = float(1. / (1 + fabs(double(tk[k] - tij))));
+                float dir = rx * gtx + ry * gty;
+                if (fabs(double(dir)) <= 0.01) dir = 0.000001f;
+                wt[k] = used[k] ? float(fabs(double(dst * lev * dir))) : 0.f;
+                L.wts[g][gl + kG * k] = wt[k];
+            }
+            SQ_T(c2);
+            for (int c0 = 0; c0 < C; c0 += kChunkC) {
+                const int nc = min(kChunkC, C - c0);
+                // the values cv2's gradient reads at this lane's positions, every channel of the chunk
+                float vv[kChunkC][2][7];
+#pragma unroll
+                for (int cc = 0; cc < kChunkC; ++cc) {
+                    const float *pl = ob + int64_t(c0 + min(cc, nc - 1)) * HW;
+#pragma unroll
+                    for (int k = 0; k < 2; ++k) {
+                        const int y = i + da[k], x = j + db[k];  // padded (k, l) of cv2's loop
+                        const int k1 = y == 1, kE = y == eh - 2, l1 = x == 1, lE = x == ew - 2;
+                        auto V = [&](int yy, int xx) -> float {  // unpadded read, clamped (unselected reads only)
+                            return pl[int64_t(min(max(yy, 0), H - 1)) * W + min(max(xx, 0), W - 1)];
+                        };
+                        vv[cc][k][0] = V(y - 1 + k1, x - 1 + l1);  // (km, lm)
+                        vv[cc][k][1] = V(y - 1 + k1, x - lE);      // (km, lp + 1)
+                        vv[cc][k][2] = V(y - 1 + k1, x - 2 + l1);  // (km, lm - 1)
+                        vv[cc][k][3] = V(y - 1 + k1, x - 1 - lE);  // (km, lp)
+                        vv[cc][k][4] = V(y - kE, x - 1 + l1);      // (kp + 1, lm)
+                        vv[cc][k][5] = V(y - 2 + k1, x - 1 + l1);  // (km - 1, lm)
+                        vv[cc][k][6] = V(y - 1 - kE, x - 1 + l1);  // (kp, lm)
+                    }
+                }
+#pragma unroll
+                for (int cc = 0; cc < kChunkC; ++cc)
+#pragma unroll
+                    for (int k = 0; k < 2; ++k) {
+                        const bool nr = !(sR[k] >= s), nl = !(sL[k] >= s), nd = !(sD[k] >= s), nu = !(sU[k] >= s);
+                        const float *v = vv[cc][k];
+                        const float vs = v[0];
+                        const float gix = nr ? (nl ? (v[1] - v[2]) * 2.0f : (v[1] - vs)) : (nl ? (v[3] - v[2]) : 0.f);
+                        const float giy = nd ? (nu ? (v[4] - v[5]) * 2.0f : (v[4] - vs)) : (nu ? (v[6] - v[5]) : 0.f);
+                        const float ry = float(-da[k]), rx = float(-db[k]);
+                        L.terms[g][cc][0][gl + kG * k] = wt[k] * vs;
+                        L.terms[g][cc][1][gl + kG * k] = wt[k] * (gix * rx);
+                        L.terms[g][cc][2][gl + kG * k] = wt[k] * (giy * ry);
+                    }
+                // the group's lanes are one wave's: LDS order within it suffices
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                if (gl < nc) {
+                    // cv2's sums in its (k, l) order, one lane per channel.  An
+                    // unused position's weight and terms are +-0: adding them
+                    // leaves every sum unchanged except the sign of an exact
+                    // zero, which the final expression cannot see.
+                    const int cc = gl;
+                    float sum = 1.0e-20f;
+#pragma unroll
+                    for (int d = 0; d < kDisk; ++d) sum += L.wts[g][d];
+                    float Ia = 0.f, Jx = 0.f, Jy = 0.f;
+#pragma unroll
+                    for (int d = 0; d < kDisk; ++d) {
+                        Ia += L.terms[g][cc][0][d];
+                        Jx -= L.terms[g][cc][1][d];
+                        Jy -= L.terms[g][cc][2][d];
+                    }
+                    const float sat = float(double(Ia / sum) +
+                                            double(Jx + Jy) / (sqrt(double(Jx * Jx + Jy * Jy)) + double(1.0e-20f)) +
+                                            double(0.5f));
+                    ob[int64_t(c0 + cc) * HW + int64_t(i - 1) * W + (j - 1)] = float(sat_u8(sat));
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+            SQ_T(c3);
+            // release the holes of larger stamp whose window holds this one
+            uint32_t old[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) old[k] = (sw[k] > s && sw[k] != INF) ? atomicSub(&m.own[qq[k]], 1u) : 0u;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (old[k] == 1u) fb[atomicAdd(&L.nnext, 1u)] = uint32_t(qq[k]);
+            SQ_T(c4);
+            SQ_ACC(3, c0, c1);
+            SQ_ACC(4, c1, c2);
+            SQ_ACC(5, c2, c3);
+            SQ_ACC(6, c3, c4);
+        }
+        SQ_T(l1);
+        sync_all();
+        SQ_T(l2);
+        SQ_ACC(0, l0, l1);
+        SQ_ACC(1, l1, l2);
+        n = L.nnext;
+        __syncthreads();
+        if (tid == 0) L.nnext = 0u;
+        uint32_t *tmp = fa;
+        fa = fb;
+        fb = tmp;
+        __syncthreads();
+    }
+    if (tid == 0) {
+        m.meta[3] = levels;
+        for (int k = 0; k < 8; ++k) m.meta[16 + k] = uint32_t(prof[k] >> 8);
+    }
 }
 
 }  // namespace
@@ -700,8 +1090,12 @@ int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float 
         hipLaunchKernelGGL(sq_fmm_kernel, dim3(unsigned(nb)), dim3(kThreads), 0, st, w);
         hipLaunchKernelGGL(sq_count_kernel, dim3(unsigned((w.ew + 63) / 64), unsigned((w.eh + 3) / 4), unsigned(nb)),
                            dim3(256), 0, st, w, r);
-        hipLaunchKernelGGL(sq_colour_kernel, dim3(unsigned(nb)), dim3(kThreads), 0, st, w, out, int(C), int(H), int(W),
-                           b0, r);
+        if (r == 3)
+            hipLaunchKernelGGL(sq_colour_g16_kernel, dim3(unsigned(nb)), dim3(kG16Threads), 0, st, w, out, int(C), int(H),
+                               int(W), b0);
+        else
+            hipLaunchKernelGGL(sq_colour_kernel, dim3(unsigned(nb)), dim3(kColThreads), 0, st, w, out, int(C), int(H),
+                               int(W), b0, r);
     }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? OFD_FW_OK : int(e);

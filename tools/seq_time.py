@@ -18,10 +18,10 @@ def a256(x):
 def seq_meta(ws, B, H, W):
     eh, ew = H + 2, W + 2
     en = eh * ew
-    pi = a256(en * 4) * 6 + a256(en * 8) * 2 + a256(eh * 4) + 256
+    pi = a256(en * 4) * 6 + a256(en * 8) * 2 + a256(eh * 4) + 32 * 4
     G = min(B, (ws.numel() - 2048) // pi)
     off = 6 * a256(G * en * 4) + 2 * a256(G * en * 8) + a256(G * eh * 4)
-    return ws[off:off + G * 8 * 4].view(torch.int32).view(G, 8).cpu().numpy()
+    return ws[off:off + G * 32 * 4].view(torch.int32).view(G, 32).cpu().numpy()
 
 
 def main():
@@ -48,6 +48,24 @@ def main():
     print("meta columns: band, pushes, level0, levels, buckets, error")
     for k in np.argsort(-m[:, 3])[:8]:
         print(k, m[k, :6].tolist())
+    eh, ew = 770, 1026
+    en = eh * ew
+    pi_ = a256(en * 4) * 6 + a256(en * 8) * 2 + a256(eh * 4) + 32 * 4
+    G = min(B, (ws.numel() - 2048) // pi_)
+    k1 = 6 * a256(G * en * 4) + a256(G * en * 8)
+    kdeep = int(np.argmax(m[:, 3]))
+    L = int(m[kdeep, 3])
+    lsz = ws[k1 + kdeep * en * 8: k1 + kdeep * en * 8 + L * 4].view(torch.int32).cpu().numpy()
+    q = np.percentile(lsz, [0, 10, 50, 90, 99, 100])
+    print(f"deepest image {kdeep}: {L} levels, level sizes p0/10/50/90/99/100 {q.tolist()}, "
+          f"levels with <=16 holes {(lsz <= 16).mean():.2f}, <=64 {(lsz <= 64).mean():.2f}; "
+          f"sum ceil(n/16) {int(np.ceil(lsz / 16).sum())}, sum ceil(n/256) {int(np.ceil(lsz / 256).sum())}")
+    if m[:, 8:24].any():  # probe build (tools/seq_probe.sh): clocks >> 8, deepest image
+        r = m[kdeep]
+        print("FMM   gather/sort/claim/push/dist/log (Mclk):", [round(x * 256 / 1e6, 2) for x in r[8:14]],
+              "sweeps", int(r[14]))
+        print("COLOUR level work/barrier/readiness, per-pixel load/weights/channels/candidates (Mclk):",
+              [round(x * 256 / 1e6, 2) for x in r[16:23]])
     print("max levels", m[:, 3].max(), "max buckets", m[:, 4].max(), "errors", int((m[:, 5] != 0).sum()))
 
 
