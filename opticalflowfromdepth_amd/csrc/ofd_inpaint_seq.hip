@@ -153,14 +153,16 @@ __device__ __forceinline__ Img image(const SqWs &w, int64_t bl) {
     return m;
 }
 
-// Workgroup barrier whose global writes are visible to every thread of the
-// workgroup afterwards: release at agent scope (atomics and stores reach L2),
-// barrier, acquire at agent scope (the CU's vector L1 is invalidated, so no
-// thread reads a line cached before another thread's update).
+// Workgroup barrier after which every thread of the workgroup sees the
+// others' global stores and atomics.  Workgroup scope suffices: an image's
+// march and colours run inside one workgroup, whose waves share one CU and
+// its vector L1 (not in threadgroup-split mode), so no L2 write-back or L1
+// invalidation is needed -- agent scope would emit both (buffer_wbl2 /
+// buffer_inv) on every level, which measured 4-7 us per load round.
 __device__ __forceinline__ void sync_all() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
 // Exclusive scan of one value per thread over the 1024-thread workgroup.
@@ -807,7 +809,7 @@ __global__ __launch_bounds__(kColThreads) void sq_colour_kernel(SqWs w, float *_
 // sums: cv2 adds the window's terms in (k, l) order, and so does the group,
 // one shuffle per term.  Release: lanes own the 60 window positions 16 apart.
 constexpr int kG = 16;
-constexpr int kG16Threads = 512;  // 170 VGPRs: two waves per SIMD
+constexpr int kG16Threads = 1024;  // <= 128 VGPRs: four waves per SIMD
 constexpr int kGroups = kG16Threads / kG;
 
 constexpr int disk_count() {
@@ -854,7 +856,7 @@ __device__ __forceinline__ void win_pos(int d, int &a, int &b) {
             }
 }
 
-constexpr int kChunkC = 4;  // channels whose values are loaded together
+constexpr int kChunkC = 3;  // channels whose values are loaded together (RGB in one round)
 
 struct G16Lds {
     uint32_t nnext;
@@ -978,6 +980,8 @@ __global__ __launch_bounds__(kG16Threads) void sq_colour_g16_kernel(SqWs w, floa
                         vv[cc][k][6] = V(y - 1 - kE, x - 1 + l1);  // (kp, lm)
                     }
                 }
+                SQ_T(cv);
+                SQ_ACC(2, c2, cv);
 #pragma unroll
                 for (int cc = 0; cc < kChunkC; ++cc)
 #pragma unroll
@@ -996,6 +1000,8 @@ __global__ __launch_bounds__(kG16Threads) void sq_colour_g16_kernel(SqWs w, floa
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                SQ_T(ct);
+                SQ_ACC(7, cv, ct);
                 if (gl < nc) {
                     // cv2's sums in its (k, l) order, one lane per channel.  An
                     // unused position's weight and terms are +-0: adding them

@@ -64,8 +64,8 @@ def main():
         r = m[kdeep]
         print("FMM   gather/sort/claim/push/dist/log (Mclk):", [round(x * 256 / 1e6, 2) for x in r[8:14]],
               "sweeps", int(r[14]))
-        print("COLOUR level work/barrier/readiness, per-pixel load/weights/channels/candidates (Mclk):",
-              [round(x * 256 / 1e6, 2) for x in r[16:23]])
+        print("COLOUR level work/barrier, per-pixel [value loads], load/weights/channels/release, [terms] (Mclk):",
+              [round(x * 256 / 1e6, 2) for x in r[16:24]])
     print("max levels", m[:, 3].max(), "max buckets", m[:, 4].max(), "errors", int((m[:, 5] != 0).sum()))
 
 
