@@ -51,6 +51,7 @@
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "ofd_fw.h"
 #include "ofd_inpaint.h"
@@ -98,12 +99,18 @@ struct SqWs {
     uint64_t *k1;
     uint32_t *rowc;  // band count / offset per padded row
     uint32_t *meta;  // kMeta words per image
-    int64_t en, eh, ew;
+    uint32_t *rec;   // radius-3 COLOUR: kRecW words per hole, indexed by push seq - band count
+    uint32_t *shd;   // radius-3 COLOUR: the image as packed uint8 channels (C <= 3), H x W words
+    uint64_t *fr2;   // radius-3 COLOUR: second frontier buffer (entries beyond the LDS capacity)
+    int64_t en, eh, ew, hw;
 };
+
+constexpr int kRecW = 40;  // record words: 32 weights (lane-major), 4 code words, dependants mask (2), weight sum, pad
 
 size_t per_image_bytes(int64_t H, int64_t W) {
     const size_t en = size_t(H + 2) * size_t(W + 2);
-    return align256(en * 4) * 6 + align256(en * 8) * 2 + align256(size_t(H + 2) * 4) + kMeta * 4;
+    return align256(en * 4) * 6 + align256(en * 8) * 2 + align256(size_t(H + 2) * 4) + kMeta * 4 +
+           en * kRecW * 4 + size_t(H) * size_t(W) * 4 + en * 8 + 3 * 256;
 }
 
 SqWs carve(void *ws, int64_t G, int64_t H, int64_t W) {
@@ -122,15 +129,19 @@ SqWs carve(void *ws, int64_t G, int64_t H, int64_t W) {
     w.k0 = reinterpret_cast<uint64_t *>(p), p += n8;
     w.k1 = reinterpret_cast<uint64_t *>(p), p += n8;
     w.rowc = reinterpret_cast<uint32_t *>(p), p += align256(size_t(G) * size_t(w.eh) * 4);
-    w.meta = reinterpret_cast<uint32_t *>(p);
+    w.meta = reinterpret_cast<uint32_t *>(p), p += align256(size_t(G) * kMeta * 4);
+    w.hw = H * W;
+    w.rec = reinterpret_cast<uint32_t *>(p), p += align256(size_t(G) * size_t(w.en) * kRecW * 4);
+    w.shd = reinterpret_cast<uint32_t *>(p), p += align256(size_t(G) * size_t(w.hw) * 4);
+    w.fr2 = reinterpret_cast<uint64_t *>(p);
     return w;
 }
 
 // One image's view of the workspace
 struct Img {
-    uint32_t *sO, *sI, *own, *logp, *rowc, *meta;
+    uint32_t *sO, *sI, *own, *logp, *rowc, *meta, *rec, *shd;
     float *t, *logt;
-    uint64_t *k0, *k1;
+    uint64_t *k0, *k1, *fr2;
     int64_t en;
     int eh, ew;
 };
@@ -147,6 +158,9 @@ __device__ __forceinline__ Img image(const SqWs &w, int64_t bl) {
     m.k1 = w.k1 + bl * w.en;
     m.rowc = w.rowc + bl * w.eh;
     m.meta = w.meta + bl * kMeta;
+    m.rec = w.rec + bl * w.en * kRecW;
+    m.shd = w.shd + bl * w.hw;
+    m.fr2 = w.fr2 + bl * w.en;
     m.en = w.en;
     m.eh = int(w.eh);
     m.ew = int(w.ew);
@@ -201,7 +215,7 @@ __device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t &total, uint
 // at the padded position.
 __global__ __launch_bounds__(256) void sq_prep_kernel(const float *__restrict__ img, const float *__restrict__ valid,
                                                       const float *__restrict__ coll, float *__restrict__ out,
-                                                      SqWs w, int C, int H, int W, int64_t b0) {
+                                                      SqWs w, int C, int H, int W, int64_t b0, int shadow) {
     const int x = blockIdx.x * 64 + (threadIdx.x & 63), y = blockIdx.y * 4 + (threadIdx.x >> 6);
     if (x >= W || y >= H) return;
     const int64_t HW = int64_t(H) * W, bl = blockIdx.z, b = b0 + bl;
@@ -222,7 +236,13 @@ __global__ __launch_bounds__(256) void sq_prep_kernel(const float *__restrict__ 
     w.sI[bl * w.en + int64_t(y + 1) * w.ew + (x + 1)] = hp != 1u ? INF : 0u;
     const float *ib = img + b * int64_t(C) * HW;
     float *ob = out + b * int64_t(C) * HW;
-    for (int c = 0; c < C; ++c) ob[c * HW + p] = float(to_u8(ib[c * HW + p]));
+    uint32_t pk = 0;
+    for (int c = 0; c < C; ++c) {
+        const unsigned u = to_u8(ib[c * HW + p]);
+        ob[c * HW + p] = float(u);
+        pk |= c < 4 ? u << (8 * c) : 0u;
+    }
+    if (shadow) w.shd[bl * w.hw + p] = pk;
 }
 
 // ---------------------------------------------------------------- INIT
@@ -1060,6 +1080,323 @@ __global__ __launch_bounds__(kG16Threads) void sq_colour_g16_kernel(SqWs w, floa
     }
 }
 
+// ---------------------------------------------------------------- radius 3, C <= 3: records + LDS frontier
+// What a hole's colour needs besides the colours themselves -- its 29 disk
+// weights, the gradient formula at each disk position, the weight sum, and
+// which later holes read it -- depends on the stamps and distances only, so
+// RECORD computes it for every hole of the chunk at once (one thread per
+// hole, no ordering).  COLOUR3 then walks the Kahn levels with one round of
+// loads per level: a 16-byte record slice and the hole's 61-pixel window of
+// packed uint8 colours (the shadow image), 8 lanes per hole, 128 holes in
+// flight, the frontier in LDS (entries past kFrCap in global memory).  The
+// release atomics are issued as soon as the record's dependants mask lands,
+// so their round trip overlaps the colour arithmetic.
+constexpr int kL3 = 8;                   // lanes per hole
+constexpr int kSlots3 = 1024 / kL3;      // holes in flight per workgroup
+constexpr int kVal3 = 61;                // window (disk dilated by 3x3) incl. the centre
+constexpr int kTerm3 = 9 * kDisk;        // 3 channels x (Ia, Jx, Jy) x disk positions
+constexpr int kFrCap = 1280;             // LDS frontier entries per buffer
+
+// e-th position (raster order) of the window including its centre
+__device__ __forceinline__ void val_pos(int e, int &a, int &b) {
+    int n = 0;
+    a = b = 0;
+    for (int u = -4; u <= 4; ++u)
+        for (int v = -4; v <= 4; ++v)
+            if (win3(u, v)) {
+                if (n == e) {
+                    a = u;
+                    b = v;
+                }
+                ++n;
+            }
+}
+
+// Record of padded hole (i, j) with stamp s (layout: word 4*l + k = weight of
+// disk position l + 8k; word 32 + l/2, bits 16*(l&1) + 4k = gradient codes of
+// that position (x in bits 0-1, y in bits 2-3); words 36-37 = dependants
+// mask over win_pos order; word 38 = cv2's weight sum).  Also the Kahn
+// counter (record index << 32 | earlier holes in the window) and level 0.
+__global__ __launch_bounds__(256) void sq_record3_kernel(SqWs w) {
+    const int j = blockIdx.x * 64 + (threadIdx.x & 63), i = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const Img m = image(w, blockIdx.z);
+    const int eh = m.eh, ew = m.ew;
+    if (i < 1 || j < 1 || i >= eh - 1 || j >= ew - 1) return;
+    const int64_t p = int64_t(i) * ew + j;
+    const uint32_t *st = m.sI;
+    const uint32_t s = st[p];
+    if (s == 0u || s == INF) return;
+    const uint32_t idx = s - m.meta[0];
+    auto at = [&](int y, int x) -> int64_t { return int64_t(min(max(y, 0), eh - 1)) * ew + min(max(x, 0), ew - 1); };
+    // Kahn counter and dependants: window positions inside the image
+    uint32_t cnt = 0;
+    uint64_t dep = 0;
+    int bit = 0;
+#pragma unroll
+    for (int a = -4; a <= 4; ++a)
+#pragma unroll
+        for (int b = -4; b <= 4; ++b) {
+            if (!win3(a, b) || !(a || b)) continue;
+            const int y = i + a, x = j + b;
+            if (y >= 1 && x >= 1 && y < eh - 1 && x < ew - 1) {
+                const uint32_t q = st[int64_t(y) * ew + x];
+                cnt += (q != 0u && q < s) ? 1u : 0u;
+                if (q > s && q != INF) dep |= uint64_t(1) << bit;
+            }
+            ++bit;
+        }
+    // cv2's distance gradient at the hole
+    const uint32_t su = st[p - ew], sd = st[p + ew], sl = st[p - 1], sr = st[p + 1];
+    const float tij = m.t[p], tu = m.t[p - ew], td = m.t[p + ew], tl = m.t[p - 1], tr = m.t[p + 1];
+    float gtx, gty;
+    if (!(sr >= s))
+        gtx = !(sl >= s) ? (tr - tl) * 0.5f : (tr - tij);
+    else
+        gtx = !(sl >= s) ? (tij - tl) : 0.f;
+    if (!(sd >= s))
+        gty = !(su >= s) ? (td - tu) * 0.5f : (td - tij);
+    else
+        gty = !(su >= s) ? (tij - tu) : 0.f;
+    uint32_t r[kRecW];
+#pragma unroll
+    for (int k = 0; k < kRecW; ++k) r[k] = 0u;
+    float sum = 1.0e-20f;
+    int d = 0;
+#pragma unroll
+    for (int a = -3; a <= 3; ++a)
+#pragma unroll
+        for (int b = -3; b <= 3; ++b) {
+            if (!disk3(a, b)) continue;
+            const int y = i + a, x = j + b;
+            const bool inimg = y > 0 && x > 0 && y < eh - 1 && x < ew - 1;
+            const bool used = inimg && !(st[at(y, x)] >= s);
+            const float ry = float(-a), rx = float(-b);
+            const float len2 = rx * rx + ry * ry;
+            const float dst = float(1. / (double(len2) * sqrt(double(len2))));
+            const float lev = float(1. / (1 + fabs(double(m.t[at(y, x)] - tij))));
+            float dir = rx * gtx + ry * gty;
+            if (fabs(double(dir)) <= 0.01) dir = 0.000001f;
+            const float wt = used ? float(fabs(double(dst * lev * dir))) : 0.f;
+            sum += wt;
+            const bool nr = !(st[at(y, x + 1)] >= s), nl = !(st[at(y, x - 1)] >= s);
+            const bool nd = !(st[at(y + 1, x)] >= s), nu = !(st[at(y - 1, x)] >= s);
+            const uint32_t cx = nr ? (nl ? 0u : 1u) : (nl ? 2u : 3u);
+            const uint32_t cy = nd ? (nu ? 0u : 1u) : (nu ? 2u : 3u);
+            const int l = d % kL3, k = d / kL3;
+            r[4 * l + k] = __float_as_uint(wt);
+            r[32 + l / 2] |= (cx | (cy << 2)) << (16 * (l & 1) + 4 * k);
+            ++d;
+        }
+    r[36] = uint32_t(dep);
+    r[37] = uint32_t(dep >> 32);
+    r[38] = __float_as_uint(sum);
+    uint4 *dstp = reinterpret_cast<uint4 *>(m.rec + size_t(idx) * kRecW);
+#pragma unroll
+    for (int k = 0; k < kRecW / 4; ++k) dstp[k] = make_uint4(r[4 * k], r[4 * k + 1], r[4 * k + 2], r[4 * k + 3]);
+    m.k1[p] = (uint64_t(idx) << 32) | cnt;
+    if (cnt == 0u) m.k0[atomicAdd(&m.meta[2], 1u)] = (uint64_t(idx) << 32) | uint64_t(p);
+}
+
+struct C3Lds {
+    uint32_t nnext;
+    uint64_t fr[2][kFrCap];
+    float buf[kSlots3][kTerm3];  // per hole: the 9x9 colour grid (81 words), then the terms
+    float res[kSlots3][9];       // per hole: chain results (Ia, Jx, Jy per channel)
+};
+
+__global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, float *__restrict__ out, int C, int H, int W,
+                                                          int64_t b0) {
+    __shared__ C3Lds L;
+    const int tid = threadIdx.x, g = tid / kL3, gl = tid % kL3;
+    const Img m = image(w, blockIdx.x);
+    const int eh = m.eh, ew = m.ew;
+    const int64_t HW = int64_t(H) * W;
+    float *ob = out + (b0 + blockIdx.x) * int64_t(C) * HW;
+    uint8_t *shb = reinterpret_cast<uint8_t *>(m.shd);
+    // this lane's window loads, dependants bits and disk positions, as 9x9
+    // grid cells (row-major, centre 40)
+    // (packed per k: window load cell | dependant cell << 8 | disk cell << 16)
+    int tb[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        int a, b;
+        val_pos(gl + kL3 * k, a, b);
+        tb[k] = (a + 4) * 9 + b + 4;
+        win_pos(gl + kL3 * k, a, b);
+        tb[k] |= ((a + 4) * 9 + b + 4) << 8;
+        if (k < 4) {
+            disk_pos(gl + kL3 * k, a, b);
+            tb[k] |= ((a + 4) * 9 + b + 4) << 16;
+        }
+    }
+#define VC(k) (tb[k] & 0xFF)
+#define WC(k) ((tb[k] >> 8) & 0xFF)
+#define DC(k) (tb[k] >> 16)
+    uint64_t *ga = m.k0, *gb = m.fr2;
+    int cur = 0;
+    uint32_t n = m.meta[2], levels = 0;
+    for (uint32_t e = tid; e < n && e < uint32_t(kFrCap); e += 1024) L.fr[0][e] = ga[e];
+    if (tid == 0) L.nnext = 0u;
+    __syncthreads();
+    const int nch = 3 * C;  // chains: (Ia, Jx, Jy) per channel
+    while (n) {
+        ++levels;
+        for (uint32_t base = 0; base < n; base += kSlots3) {
+            // keep the lane tables opaque, so the compiler does not hoist
+            // their derived offsets out of the loop (register pressure)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) asm volatile("" : "+v"(tb[k]));
+            const uint32_t e = base + g;
+            const bool act = e < n;
+            uint64_t ent = 0;
+            if (act) ent = e < uint32_t(kFrCap) ? L.fr[cur][e] : ga[e];
+            const uint32_t idx = uint32_t(ent >> 32), p = uint32_t(ent);
+            const int i = int(p / uint32_t(ew)), j = int(p - uint32_t(i) * uint32_t(ew));
+            // the level's one round of loads
+            const uint32_t *rp = m.rec + size_t(idx) * kRecW;
+            uint4 wq = make_uint4(0, 0, 0, 0), cq = wq, mq = wq;
+            uint32_t v[8];
+            if (act) {
+                wq = *reinterpret_cast<const uint4 *>(rp + 4 * gl);
+                cq = *reinterpret_cast<const uint4 *>(rp + 32);
+                mq = *reinterpret_cast<const uint4 *>(rp + 36);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const int y = min(max(i - 5 + VC(k) / 9, 0), H - 1), x = min(max(j - 5 + VC(k) % 9, 0), W - 1);
+                    v[k] = (gl + kL3 * k < kVal3) ? m.shd[int64_t(y) * W + x] : 0u;
+                }
+            }
+            // release the later holes that read this one (their counters
+            // reach zero only after this level's barrier is passed)
+            const uint64_t dep = uint64_t(mq.x) | (uint64_t(mq.y) << 32);
+            uint64_t old[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                old[k] = 0;
+                if (act && gl + kL3 * k < kWin && ((dep >> (gl + kL3 * k)) & 1u)) {
+                    const int64_t q = int64_t(p) + int64_t(WC(k) / 9 - 4) * ew + (WC(k) % 9 - 4);
+                    old[k] = atomicAdd(reinterpret_cast<unsigned long long *>(&m.k1[q]), ~0ull);
+                }
+            }
+            float *bf = L.buf[g];
+            uint32_t *gv = reinterpret_cast<uint32_t *>(bf);
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                if (gl + kL3 * k < kVal3) gv[VC(k)] = v[k];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // this lane's terms (disk positions gl + 8k): channels 1 and 2 go
+            // to LDS at once (past the grid), channel 0 waits in registers
+            // until every lane of the hole is done with the grid
+            const uint32_t wts[4] = {wq.x, wq.y, wq.z, wq.w};
+            const uint32_t cw = (gl >> 1) == 0 ? cq.x : (gl >> 1) == 1 ? cq.y : (gl >> 1) == 2 ? cq.z : cq.w;
+            const uint32_t codes = cw >> (16 * (gl & 1));
+            float t0[4][3];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int a = DC(k) / 9 - 4, b = DC(k) % 9 - 4, y = i + a, x = j + b;
+                const int k1 = y == 1, kE = y == eh - 2, l1 = x == 1, lE = x == ew - 2;
+                auto G = [&](int ry, int rx) -> uint32_t {  // colour word at window offset (ry, rx), clamped
+                    return gv[(min(max(ry, -4), 4) + 4) * 9 + min(max(rx, -4), 4) + 4];
+                };
+                const uint32_t w0 = G(a + k1, b + l1), w1 = G(a + k1, b + 1 - lE), w2 = G(a + k1, b - 1 + l1),
+                               w3 = G(a + k1, b - lE), w4 = G(a + 1 - kE, b + l1), w5 = G(a - 1 + k1, b + l1),
+                               w6 = G(a - kE, b + l1);
+                const float wt = __uint_as_float(wts[k]);
+                const uint32_t cx = (codes >> (4 * k)) & 3u, cy = (codes >> (4 * k + 2)) & 3u;
+                const float ry = float(-a), rx = float(-b);
+                const bool live = gl + kL3 * k < kDisk;
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    auto ch = [&](uint32_t q) -> float { return float((q >> (8 * c)) & 0xFFu); };
+                    const float vs = ch(w0);
+                    const float gix = cx == 0u ? (ch(w1) - ch(w2)) * 2.0f
+                                    : cx == 1u ? (ch(w1) - vs) : cx == 2u ? (ch(w3) - ch(w2)) : 0.f;
+                    const float giy = cy == 0u ? (ch(w4) - ch(w5)) * 2.0f
+                                    : cy == 1u ? (ch(w4) - vs) : cy == 2u ? (ch(w6) - ch(w5)) : 0.f;
+                    const float ta = wt * vs, tx = wt * (gix * rx), ty = wt * (giy * ry);
+                    if (c == 0) {
+                        t0[k][0] = ta;
+                        t0[k][1] = tx;
+                        t0[k][2] = ty;
+                    } else if (live && c < C) {
+                        bf[(3 * c) * kDisk + gl + kL3 * k] = ta;
+                        bf[(3 * c + 1) * kDisk + gl + kL3 * k] = tx;
+                        bf[(3 * c + 2) * kDisk + gl + kL3 * k] = ty;
+                    }
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (gl + kL3 * k < kDisk)
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) bf[q * kDisk + gl + kL3 * k] = t0[k][q];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // cv2's sums in its (k, l) order, one chain per lane
+            for (int cn = gl; cn < nch; cn += kL3) {
+                const float *tc = bf + cn * kDisk;
+                float acc = 0.f;
+                if (cn % 3 == 0) {
+#pragma unroll
+                    for (int q = 0; q < kDisk; ++q) acc += tc[q];
+                } else {
+#pragma unroll
+                    for (int q = 0; q < kDisk; ++q) acc -= tc[q];
+                }
+                L.res[g][cn] = acc;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (act && gl < C) {
+                const float sum = __uint_as_float(mq.z);
+                const float Ia = L.res[g][3 * gl], Jx = L.res[g][3 * gl + 1], Jy = L.res[g][3 * gl + 2];
+                const float sat = float(double(Ia / sum) +
+                                        double(Jx + Jy) / (sqrt(double(Jx * Jx + Jy * Jy)) + double(1.0e-20f)) +
+                                        double(0.5f));
+                const unsigned u = sat_u8(sat);
+                const int64_t q = int64_t(i - 1) * W + (j - 1);
+                ob[int64_t(gl) * HW + q] = float(u);
+                shb[4 * q + gl] = uint8_t(u);
+            }
+            // holes whose last earlier neighbour this was join the next level
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                if (uint32_t(old[k]) == 1u) {
+                    const uint32_t f = atomicAdd(&L.nnext, 1u);
+                    const int64_t q = int64_t(p) + int64_t(WC(k) / 9 - 4) * ew + (WC(k) % 9 - 4);
+                    const uint64_t en = (old[k] & 0xFFFFFFFF00000000ull) | uint64_t(q);
+                    if (f < uint32_t(kFrCap))
+                        L.fr[cur ^ 1][f] = en;
+                    else
+                        gb[f] = en;
+                }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        sync_all();
+        n = L.nnext;
+        __syncthreads();
+        if (tid == 0) L.nnext = 0u;
+        cur ^= 1;
+        uint64_t *tmp = ga;
+        ga = gb;
+        gb = tmp;
+        __syncthreads();
+    }
+    if (tid == 0) m.meta[3] = levels;
+}
+#undef VC
+#undef WC
+#undef DC
+
 }  // namespace
 
 extern "C" {
@@ -1086,14 +1423,27 @@ int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float 
     if (G > B) G = B;
     hipStream_t st = static_cast<hipStream_t>(stream);
     const SqWs w = carve(workspace, G, H, W);
+    // radius 3 with up to 3 channels (utils.inpaint's RGB call): the record
+    // path; OFD_SEQ_COLOUR=g16 selects the one-pass colour kernel (A/B)
+    static const bool force_g16 = [] {
+        const char *e = getenv("OFD_SEQ_COLOUR");
+        return e && e[0] == 'g';
+    }();
+    const bool rec3 = r == 3 && C <= 3 && !force_g16;
     for (int64_t b0 = 0; b0 < B; b0 += G) {
         const int64_t nb = B - b0 < G ? B - b0 : G;
         hipLaunchKernelGGL(sq_prep_kernel, dim3(unsigned((W + 63) / 64), unsigned((H + 3) / 4), unsigned(nb)), dim3(256),
-                           0, st, img, valid, collision, out, w, int(C), int(H), int(W), b0);
+                           0, st, img, valid, collision, out, w, int(C), int(H), int(W), b0, rec3 ? 1 : 0);
         hipLaunchKernelGGL(sq_init_kernel, dim3(unsigned((w.eh + 3) / 4), unsigned(nb)), dim3(256), 0, st, w, r);
         hipLaunchKernelGGL(sq_band_scan_kernel, dim3(unsigned(nb)), dim3(kThreads), 0, st, w);
         hipLaunchKernelGGL(sq_band_write_kernel, dim3(unsigned((w.eh + 3) / 4), unsigned(nb)), dim3(256), 0, st, w);
         hipLaunchKernelGGL(sq_fmm_kernel, dim3(unsigned(nb)), dim3(kThreads), 0, st, w);
+        if (rec3) {
+            hipLaunchKernelGGL(sq_record3_kernel, dim3(unsigned((w.ew + 63) / 64), unsigned((w.eh + 3) / 4), unsigned(nb)),
+                               dim3(256), 0, st, w);
+            hipLaunchKernelGGL(sq_colour3_kernel, dim3(unsigned(nb)), dim3(1024), 0, st, w, out, int(C), int(H), int(W), b0);
+            continue;
+        }
         hipLaunchKernelGGL(sq_count_kernel, dim3(unsigned((w.ew + 63) / 64), unsigned((w.eh + 3) / 4), unsigned(nb)),
                            dim3(256), 0, st, w, r);
         if (r == 3)

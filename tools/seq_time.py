@@ -18,7 +18,7 @@ def a256(x):
 def seq_meta(ws, B, H, W):
     eh, ew = H + 2, W + 2
     en = eh * ew
-    pi = a256(en * 4) * 6 + a256(en * 8) * 2 + a256(eh * 4) + 32 * 4
+    pi = a256(en * 4) * 6 + a256(en * 8) * 2 + a256(eh * 4) + 32 * 4 + en * 160 + H * W * 4 + en * 8 + 768
     G = min(B, (ws.numel() - 2048) // pi)
     off = 6 * a256(G * en * 4) + 2 * a256(G * en * 8) + a256(G * eh * 4)
     return ws[off:off + G * 32 * 4].view(torch.int32).view(G, 32).cpu().numpy()
@@ -50,11 +50,15 @@ def main():
         print(k, m[k, :6].tolist())
     eh, ew = 770, 1026
     en = eh * ew
-    pi_ = a256(en * 4) * 6 + a256(en * 8) * 2 + a256(eh * 4) + 32 * 4
+    pi_ = a256(en * 4) * 6 + a256(en * 8) * 2 + a256(eh * 4) + 32 * 4 + en * 160 + 768 * 1024 * 4 + en * 8 + 768
     G = min(B, (ws.numel() - 2048) // pi_)
     k1 = 6 * a256(G * en * 4) + a256(G * en * 8)
     kdeep = int(np.argmax(m[:, 3]))
     L = int(m[kdeep, 3])
+    if not os.environ.get("OFD_SEQ_COLOUR", "").startswith("g"):  # level sizes: the g16 colour kernel only
+        print(f"deepest image {kdeep}: {L} levels")
+        print("max levels", m[:, 3].max(), "max buckets", m[:, 4].max(), "errors", int((m[:, 5] != 0).sum()))
+        return
     lsz = ws[k1 + kdeep * en * 8: k1 + kdeep * en * 8 + L * 4].view(torch.int32).cpu().numpy()
     q = np.percentile(lsz, [0, 10, 50, 90, 99, 100])
     print(f"deepest image {kdeep}: {L} levels, level sizes p0/10/50/90/99/100 {q.tolist()}, "
