@@ -239,8 +239,10 @@ __global__ __launch_bounds__(256) void sq_prep_kernel(const float *__restrict__ 
     uint32_t pk = 0;
     for (int c = 0; c < C; ++c) {
         const unsigned u = to_u8(ib[c * HW + p]);
-        ob[c * HW + p] = float(u);
-        pk |= c < 4 ? u << (8 * c) : 0u;
+        if (shadow)
+            pk |= u << (8 * c);  // C <= 3; sq_unpack_kernel writes out
+        else
+            ob[c * HW + p] = float(u);
     }
     if (shadow) w.shd[bl * w.hw + p] = pk;
 }
@@ -1116,7 +1118,7 @@ __device__ __forceinline__ void val_pos(int e, int &a, int &b) {
 // disk position l + 8k; word 32 + l/2, bits 16*(l&1) + 4k = gradient codes of
 // that position (x in bits 0-1, y in bits 2-3); words 36-37 = dependants
 // mask over win_pos order; word 38 = cv2's weight sum).  Also the Kahn
-// counter (record index << 32 | earlier holes in the window) and level 0.
+// counter (record index << 6 | earlier holes in the window) and level 0.
 __global__ __launch_bounds__(256) void sq_record3_kernel(SqWs w) {
     const int j = blockIdx.x * 64 + (threadIdx.x & 63), i = blockIdx.y * 4 + (threadIdx.x >> 6);
     const Img m = image(w, blockIdx.z);
@@ -1193,7 +1195,7 @@ __global__ __launch_bounds__(256) void sq_record3_kernel(SqWs w) {
     uint4 *dstp = reinterpret_cast<uint4 *>(m.rec + size_t(idx) * kRecW);
 #pragma unroll
     for (int k = 0; k < kRecW / 4; ++k) dstp[k] = make_uint4(r[4 * k], r[4 * k + 1], r[4 * k + 2], r[4 * k + 3]);
-    m.k1[p] = (uint64_t(idx) << 32) | cnt;
+    m.own[p] = (idx << 6) | cnt;  // cnt <= 60; idx < 2^26 (the launcher's bound)
     if (cnt == 0u) m.k0[atomicAdd(&m.meta[2], 1u)] = (uint64_t(idx) << 32) | uint64_t(p);
 }
 
@@ -1204,14 +1206,11 @@ struct C3Lds {
     float res[kSlots3][9];       // per hole: chain results (Ia, Jx, Jy per channel)
 };
 
-__global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, float *__restrict__ out, int C, int H, int W,
-                                                          int64_t b0) {
+__global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, int C, int H, int W) {
     __shared__ C3Lds L;
     const int tid = threadIdx.x, g = tid / kL3, gl = tid % kL3;
     const Img m = image(w, blockIdx.x);
     const int eh = m.eh, ew = m.ew;
-    const int64_t HW = int64_t(H) * W;
-    float *ob = out + (b0 + blockIdx.x) * int64_t(C) * HW;
     uint8_t *shb = reinterpret_cast<uint8_t *>(m.shd);
     // this lane's window loads, dependants bits and disk positions, as 9x9
     // grid cells (row-major, centre 40)
@@ -1239,9 +1238,14 @@ __global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, float *__restr
     if (tid == 0) L.nnext = 0u;
     __syncthreads();
     const int nch = 3 * C;  // chains: (Ia, Jx, Jy) per channel
+    uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    (void)prof;
     while (n) {
         ++levels;
+        SQ_T(l0);
         for (uint32_t base = 0; base < n; base += kSlots3) {
+            if (base + uint32_t(tid / 64) * (64 / kL3) >= n) continue;  // no hole of this round in this wave
+            SQ_T(c0);
             // keep the lane tables opaque, so the compiler does not hoist
             // their derived offsets out of the loop (register pressure)
 #pragma unroll
@@ -1266,18 +1270,20 @@ __global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, float *__restr
                     v[k] = (gl + kL3 * k < kVal3) ? m.shd[int64_t(y) * W + x] : 0u;
                 }
             }
+            SQ_T(c0a);
             // release the later holes that read this one (their counters
             // reach zero only after this level's barrier is passed)
             const uint64_t dep = uint64_t(mq.x) | (uint64_t(mq.y) << 32);
-            uint64_t old[8];
+            uint32_t old[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 old[k] = 0;
                 if (act && gl + kL3 * k < kWin && ((dep >> (gl + kL3 * k)) & 1u)) {
                     const int64_t q = int64_t(p) + int64_t(WC(k) / 9 - 4) * ew + (WC(k) % 9 - 4);
-                    old[k] = atomicAdd(reinterpret_cast<unsigned long long *>(&m.k1[q]), ~0ull);
+                    old[k] = atomicSub(&m.own[q], 1u);
                 }
             }
+            SQ_T(c1);
             float *bf = L.buf[g];
             uint32_t *gv = reinterpret_cast<uint32_t *>(bf);
 #pragma unroll
@@ -1297,30 +1303,33 @@ __global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, float *__restr
             for (int k = 0; k < 4; ++k) {
                 const int a = DC(k) / 9 - 4, b = DC(k) % 9 - 4, y = i + a, x = j + b;
                 const int k1 = y == 1, kE = y == eh - 2, l1 = x == 1, lE = x == ew - 2;
-                auto G = [&](int ry, int rx) -> uint32_t {  // colour word at window offset (ry, rx), clamped
-                    return gv[(min(max(ry, -4), 4) + 4) * 9 + min(max(rx, -4), 4) + 4];
+                auto G = [&](int ry, int rx) -> uint32_t {  // colour word at window offset (ry, rx), |ry|, |rx| <= 4
+                    return gv[(ry + 4) * 9 + rx + 4];
                 };
                 const uint32_t w0 = G(a + k1, b + l1), w1 = G(a + k1, b + 1 - lE), w2 = G(a + k1, b - 1 + l1),
                                w3 = G(a + k1, b - lE), w4 = G(a + 1 - kE, b + l1), w5 = G(a - 1 + k1, b + l1),
                                w6 = G(a - kE, b + l1);
                 const float wt = __uint_as_float(wts[k]);
                 const uint32_t cx = (codes >> (4 * k)) & 3u, cy = (codes >> (4 * k + 2)) & 3u;
+                // cv2's gradient cases as (A - B) * f, selected once for all channels:
+                // code 0: (v1 - v2) * 2, 1: (v1 - v0), 2: (v3 - v2), 3: none ((v0 - v0) * 0 = +0)
+                const uint32_t xa = cx <= 1u ? w1 : (cx == 2u ? w3 : w0), xb = (cx & 1u) ? w0 : w2;
+                const uint32_t ya = cy <= 1u ? w4 : (cy == 2u ? w6 : w0), yb = (cy & 1u) ? w0 : w5;
+                const float fx = cx == 0u ? 2.0f : (cx == 3u ? 0.0f : 1.0f);
+                const float fy = cy == 0u ? 2.0f : (cy == 3u ? 0.0f : 1.0f);
                 const float ry = float(-a), rx = float(-b);
                 const bool live = gl + kL3 * k < kDisk;
 #pragma unroll
                 for (int c = 0; c < 3; ++c) {
                     auto ch = [&](uint32_t q) -> float { return float((q >> (8 * c)) & 0xFFu); };
                     const float vs = ch(w0);
-                    const float gix = cx == 0u ? (ch(w1) - ch(w2)) * 2.0f
-                                    : cx == 1u ? (ch(w1) - vs) : cx == 2u ? (ch(w3) - ch(w2)) : 0.f;
-                    const float giy = cy == 0u ? (ch(w4) - ch(w5)) * 2.0f
-                                    : cy == 1u ? (ch(w4) - vs) : cy == 2u ? (ch(w6) - ch(w5)) : 0.f;
+                    const float gix = (ch(xa) - ch(xb)) * fx, giy = (ch(ya) - ch(yb)) * fy;
                     const float ta = wt * vs, tx = wt * (gix * rx), ty = wt * (giy * ry);
                     if (c == 0) {
                         t0[k][0] = ta;
                         t0[k][1] = tx;
                         t0[k][2] = ty;
-                    } else if (live && c < C) {
+                    } else if (live) {  // chains past 3 * C are never summed
                         bf[(3 * c) * kDisk + gl + kL3 * k] = ta;
                         bf[(3 * c + 1) * kDisk + gl + kL3 * k] = tx;
                         bf[(3 * c + 2) * kDisk + gl + kL3 * k] = ty;
@@ -1338,6 +1347,7 @@ __global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, float *__restr
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            SQ_T(c2);
             // cv2's sums in its (k, l) order, one chain per lane
             for (int cn = gl; cn < nch; cn += kL3) {
                 const float *tc = bf + cn * kDisk;
@@ -1354,6 +1364,7 @@ __global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, float *__restr
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            SQ_T(c3);
             if (act && gl < C) {
                 const float sum = __uint_as_float(mq.z);
                 const float Ia = L.res[g][3 * gl], Jx = L.res[g][3 * gl + 1], Jy = L.res[g][3 * gl + 2];
@@ -1361,17 +1372,15 @@ __global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, float *__restr
                                         double(Jx + Jy) / (sqrt(double(Jx * Jx + Jy * Jy)) + double(1.0e-20f)) +
                                         double(0.5f));
                 const unsigned u = sat_u8(sat);
-                const int64_t q = int64_t(i - 1) * W + (j - 1);
-                ob[int64_t(gl) * HW + q] = float(u);
-                shb[4 * q + gl] = uint8_t(u);
+                shb[4 * (int64_t(i - 1) * W + (j - 1)) + gl] = uint8_t(u);
             }
             // holes whose last earlier neighbour this was join the next level
 #pragma unroll
             for (int k = 0; k < 8; ++k)
-                if (uint32_t(old[k]) == 1u) {
+                if ((old[k] & 63u) == 1u) {
                     const uint32_t f = atomicAdd(&L.nnext, 1u);
                     const int64_t q = int64_t(p) + int64_t(WC(k) / 9 - 4) * ew + (WC(k) % 9 - 4);
-                    const uint64_t en = (old[k] & 0xFFFFFFFF00000000ull) | uint64_t(q);
+                    const uint64_t en = (uint64_t(old[k] >> 6) << 32) | uint64_t(q);
                     if (f < uint32_t(kFrCap))
                         L.fr[cur ^ 1][f] = en;
                     else
@@ -1380,8 +1389,18 @@ __global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, float *__restr
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            SQ_T(c4);
+            SQ_ACC(2, c0, c0a);
+            SQ_ACC(6, c0a, c1);
+            SQ_ACC(3, c1, c2);
+            SQ_ACC(4, c2, c3);
+            SQ_ACC(5, c3, c4);
         }
+        SQ_T(l1);
         sync_all();
+        SQ_T(l2);
+        SQ_ACC(0, l0, l1);
+        SQ_ACC(1, l1, l2);
         n = L.nnext;
         __syncthreads();
         if (tid == 0) L.nnext = 0u;
@@ -1391,11 +1410,24 @@ __global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, float *__restr
         gb = tmp;
         __syncthreads();
     }
-    if (tid == 0) m.meta[3] = levels;
+    if (tid == 0) {
+        m.meta[3] = levels;
+        for (int k = 0; k < 8; ++k) m.meta[16 + k] = uint32_t(prof[k] >> 8);
+    }
 }
 #undef VC
 #undef WC
 #undef DC
+
+// The record path's result: every pixel's colours from the shadow image
+// (kept pixels hold PREP's uint8 cast, holes their fill), as float32.
+__global__ __launch_bounds__(256) void sq_unpack_kernel(SqWs w, float *__restrict__ out, int C, int64_t HW, int64_t b0) {
+    const int64_t p = int64_t(blockIdx.x) * 256 + threadIdx.x;
+    if (p >= HW) return;
+    const uint32_t v = w.shd[int64_t(blockIdx.y) * w.hw + p];
+    float *ob = out + (b0 + blockIdx.y) * int64_t(C) * HW + p;
+    for (int c = 0; c < C; ++c) ob[int64_t(c) * HW] = float((v >> (8 * c)) & 0xFFu);
+}
 
 }  // namespace
 
@@ -1429,7 +1461,7 @@ int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float 
         const char *e = getenv("OFD_SEQ_COLOUR");
         return e && e[0] == 'g';
     }();
-    const bool rec3 = r == 3 && C <= 3 && !force_g16;
+    const bool rec3 = r == 3 && C <= 3 && en < (int64_t(1) << 26) && !force_g16;
     for (int64_t b0 = 0; b0 < B; b0 += G) {
         const int64_t nb = B - b0 < G ? B - b0 : G;
         hipLaunchKernelGGL(sq_prep_kernel, dim3(unsigned((W + 63) / 64), unsigned((H + 3) / 4), unsigned(nb)), dim3(256),
@@ -1441,7 +1473,9 @@ int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float 
         if (rec3) {
             hipLaunchKernelGGL(sq_record3_kernel, dim3(unsigned((w.ew + 63) / 64), unsigned((w.eh + 3) / 4), unsigned(nb)),
                                dim3(256), 0, st, w);
-            hipLaunchKernelGGL(sq_colour3_kernel, dim3(unsigned(nb)), dim3(1024), 0, st, w, out, int(C), int(H), int(W), b0);
+            hipLaunchKernelGGL(sq_colour3_kernel, dim3(unsigned(nb)), dim3(1024), 0, st, w, int(C), int(H), int(W));
+            hipLaunchKernelGGL(sq_unpack_kernel, dim3(unsigned((H * W + 255) / 256), unsigned(nb)), dim3(256), 0, st, w,
+                               out, int(C), int64_t(H * W), b0);
             continue;
         }
         hipLaunchKernelGGL(sq_count_kernel, dim3(unsigned((w.ew + 63) / 64), unsigned((w.eh + 3) / 4), unsigned(nb)),

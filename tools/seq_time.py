@@ -57,6 +57,12 @@ def main():
     L = int(m[kdeep, 3])
     if not os.environ.get("OFD_SEQ_COLOUR", "").startswith("g"):  # level sizes: the g16 colour kernel only
         print(f"deepest image {kdeep}: {L} levels")
+        if m[:, 8:24].any():
+            r = m[kdeep]
+            print("FMM   gather/sort/claim/push/dist/log (Mclk):", [round(x * 256 / 1e6, 2) for x in r[8:14]],
+                  "sweeps", int(r[14]))
+            print("COLOUR3 level work/barrier, per-round loads/terms/chains/final+append/atomics (Mclk):",
+                  [round(x * 256 / 1e6, 2) for x in r[16:23]])
         print("max levels", m[:, 3].max(), "max buckets", m[:, 4].max(), "errors", int((m[:, 5] != 0).sum()))
         return
     lsz = ws[k1 + kdeep * en * 8: k1 + kdeep * en * 8 + L * 4].view(torch.int32).cpu().numpy()
