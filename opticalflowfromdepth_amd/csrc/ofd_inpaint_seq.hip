@@ -326,10 +326,17 @@ __global__ __launch_bounds__(256) void sq_band_write_kernel(SqWs w) {
 }
 
 // ---------------------------------------------------------------- FMM
+constexpr int kHash = 1024;  // distinct-distance sort of large buckets: hash slots
+constexpr int kMaxD = 256;   // ... and distinct distances it handles (else the merge sort)
+
 struct FmmLds {
     uint64_t keys[kCap];
     uint32_t scr[40];
     uint32_t tmin, tmax, chg;
+    uint32_t hk[kHash], hd[kHash], hc[kHash];  // distinct distance, its rank, its count
+    uint32_t wc[kThreads / 64][kMaxD];         // per wave: keys of each rank in the current chunk
+    uint32_t base[kMaxD], dv[kMaxD];
+    uint32_t nd, ovf;
 };
 
 __device__ __forceinline__ uint32_t bucket_of(float T) { return uint32_t(T * 2.0f); }
@@ -374,6 +381,123 @@ __device__ __forceinline__ uint32_t lower_bound64(const uint64_t *a, uint32_t n,
             hi = mid;
     }
     return lo;
+}
+
+__device__ __forceinline__ uint32_t hslot0(uint32_t v) { return (v * 2654435761u) >> 22; }  // kHash = 1024
+
+__device__ __forceinline__ uint32_t hfind(const FmmLds &L, uint32_t v) {
+    uint32_t h = hslot0(v);
+    while (L.hk[h] != v) h = (h + 1) & (kHash - 1);
+    return h;
+}
+
+// Stable sort of n keys (distance bits << 32 | log index, in log index order)
+// by distance when the bucket holds at most kMaxD distinct distances -- the
+// big early buckets hold a handful (0.7071, 1, ...): count the distinct
+// values in an LDS hash set, rank them, and scatter the keys in order, one
+// 1024-key chunk at a time (rank within a value = earlier lanes of the wave
+// with that value + earlier waves + earlier chunks).  Returns false, having
+// written nothing, when there are more distinct values.
+__device__ bool digit_sort(const uint64_t *g, uint64_t *out, uint32_t n, FmmLds &L) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (int i = tid; i < kHash; i += kThreads) {
+        L.hk[i] = INF;
+        L.hc[i] = 0u;
+    }
+    if (tid == 0) {
+        L.nd = 0u;
+        L.ovf = 0u;
+    }
+    __syncthreads();
+    for (uint32_t b = 0; b < n; b += kThreads) {
+        const uint32_t e = b + tid;
+        const bool in = e < n;
+        const uint32_t T = in ? uint32_t(g[e] >> 32) : INF;
+        uint64_t todo = __ballot(in);
+        while (todo) {
+            const int ld = __ffsll((unsigned long long)todo) - 1;
+            const uint32_t v = __shfl(T, ld);
+            const uint64_t mk = __ballot(in && T == v);
+            if (lane == ld) {
+                uint32_t h = hslot0(v);
+                bool ok = false;
+                for (int probe = 0; probe < kHash; ++probe) {
+                    const uint32_t prev = atomicCAS(&L.hk[h], INF, v);
+                    if (prev == INF) {
+                        const uint32_t d = atomicAdd(&L.nd, 1u);
+                        if (d < uint32_t(kMaxD)) L.dv[d] = v;
+                    }
+                    if (prev == INF || prev == v) {
+                        ok = true;
+                        break;
+                    }
+                    h = (h + 1) & (kHash - 1);
+                }
+                if (ok)
+                    atomicAdd(&L.hc[h], uint32_t(__popcll(mk)));
+                else
+                    L.ovf = 1u;
+            }
+            todo &= ~mk;
+        }
+    }
+    __syncthreads();
+    const uint32_t nd = L.nd;
+    if (L.ovf || nd > uint32_t(kMaxD)) return false;  // uniform
+    uint32_t rk = 0, v = 0;
+    if (uint32_t(tid) < nd) {
+        v = L.dv[tid];
+        for (uint32_t j = 0; j < nd; ++j) rk += L.dv[j] < v ? 1u : 0u;  // T >= 0: bits order as values
+        L.base[rk] = L.hc[hfind(L, v)];
+    }
+    __syncthreads();
+    uint32_t tot;
+    const uint32_t ex = block_scan(uint32_t(tid) < nd ? L.base[tid] : 0u, tot, L.scr);
+    if (uint32_t(tid) < nd) {
+        L.base[tid] = ex;
+        L.hd[hfind(L, v)] = rk;
+    }
+    __syncthreads();
+    const uint64_t below = (uint64_t(1) << lane) - 1;
+    for (uint32_t b = 0; b < n; b += kThreads) {
+        const uint32_t e = b + tid;
+        const bool in = e < n;
+        const uint64_t key = in ? g[e] : 0;
+        const uint32_t T = uint32_t(key >> 32);
+        for (uint32_t k = lane; k < nd; k += 64) L.wc[wave][k] = 0u;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        uint32_t d = 0, r = 0;
+        uint64_t todo = __ballot(in);
+        while (todo) {
+            const int ld = __ffsll((unsigned long long)todo) - 1;
+            const uint32_t vv = __shfl(T, ld);
+            const uint64_t mk = __ballot(in && T == vv);
+            const uint32_t dd = L.hd[hfind(L, vv)];
+            if (in && T == vv) {
+                d = dd;
+                r = uint32_t(__popcll(mk & below));
+            }
+            if (lane == ld) L.wc[wave][dd] = uint32_t(__popcll(mk));
+            todo &= ~mk;
+        }
+        __syncthreads();
+        if (in) {
+            uint32_t pre = 0;
+            for (int w2 = 0; w2 < wave; ++w2) pre += L.wc[w2][d];
+            out[L.base[d] + pre + r] = key;
+        }
+        __syncthreads();
+        if (uint32_t(tid) < nd) {
+            uint32_t sum = 0;
+#pragma unroll
+            for (int w2 = 0; w2 < kThreads / 64; ++w2) sum += L.wc[w2][tid];
+            L.base[tid] += sum;
+        }
+        __syncthreads();
+    }
+    return true;
 }
 
 // Sort n > kCap keys held in g[0, n): LDS-sorted runs of kCap, then merge
@@ -475,7 +599,7 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
         if (n > kCap) {
             for (int i = tid; i < kCap; i += kThreads) m.k0[i] = L.keys[i];
             sync_all();
-            keys = uniform ? m.k0 : global_sort(m.k0, m.k1, n, L);
+            keys = uniform ? m.k0 : (digit_sort(m.k0, m.k1, n, L) ? m.k1 : global_sort(m.k0, m.k1, n, L));
         } else if (!uniform && n > 1) {
             if (n <= 512) {
                 // rank sort (unique keys): each key's place is the number of
@@ -609,6 +733,7 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
             sync_all();
             SQ_T(f6a);
             SQ_ACC(5, f5a, f6a);
+            if (n > uint32_t(kCap)) SQ_ACC(7, f1, f6a);
             continue;
         }
         for (uint32_t it = 0;; ++it) {
@@ -642,6 +767,7 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
         sync_all();
         SQ_T(f6);
         SQ_ACC(5, f5, f6);
+        SQ_ACC(7, f1, f6);  // buckets past the LDS capacities
     }
     return seq;
 }
