@@ -331,6 +331,7 @@ constexpr int kMaxD = 256;   // ... and distinct distances it handles (else the 
 
 struct FmmLds {
     uint64_t keys[kCap];
+    uint64_t keys2[kCap];  // LDS sort ping-pong
     uint32_t scr[40];
     uint32_t tmin, tmax, chg;
     uint32_t hk[kHash], hd[kHash], hc[kHash];  // distinct distance, its rank, its count
@@ -369,6 +370,56 @@ __device__ void lds_bitonic(uint64_t *s, int m) {
             }
             __syncthreads();
         }
+}
+
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int j) {
+    const uint32_t lo = __shfl_xor(uint32_t(v), j), hi = __shfl_xor(uint32_t(v >> 32), j);
+    return (uint64_t(hi) << 32) | lo;
+}
+
+// bitonic sort of one key per lane over the wave, ascending
+__device__ __forceinline__ uint64_t wave_sort64(uint64_t v, int lane) {
+#pragma unroll
+    for (int k = 2; k <= 64; k <<= 1)
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const uint64_t o = shfl_xor64(v, j);
+            const bool keep_min = ((lane & j) == 0) == ((lane & k) == 0);
+            v = keep_min ? (o < v ? o : v) : (o > v ? o : v);
+        }
+    return v;
+}
+
+__device__ __forceinline__ uint32_t lower_bound64(const uint64_t *a, uint32_t n, uint64_t key);
+
+// Sort keys[0, n) (unique), 1 < n <= kCap, in LDS: 64-key runs sorted in
+// registers (wave shuffles, no barrier), then merge passes between the two
+// LDS buffers (each key's place = its rank in its run + its rank in the
+// partner run).  Returns the buffer holding the result.
+__device__ uint64_t *lds_sort(FmmLds &L, uint32_t n) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint64_t *src = L.keys, *dst = L.keys2;
+    for (uint32_t c = wave; c * 64 < n; c += kThreads / 64) {
+        const uint32_t i = c * 64 + lane;
+        uint64_t v = i < n ? src[i] : ~uint64_t(0);
+        v = wave_sort64(v, lane);
+        if (i < n) src[i] = v;
+    }
+    __syncthreads();
+    for (uint32_t wdt = 64; wdt < n; wdt <<= 1) {
+        for (uint32_t i = tid; i < n; i += kThreads) {
+            const uint32_t lo = i / (2 * wdt) * (2 * wdt), mid = min(lo + wdt, n), hi = min(lo + 2 * wdt, n);
+            const uint64_t key = src[i];
+            const uint32_t pos = i < mid ? (i - lo) + lower_bound64(src + mid, hi - mid, key)
+                                         : (i - mid) + lower_bound64(src + lo, mid - lo, key);
+            dst[lo + pos] = key;
+        }
+        __syncthreads();
+        uint64_t *tmp = src;
+        src = dst;
+        dst = tmp;
+    }
+    return src;
 }
 
 __device__ __forceinline__ uint32_t lower_bound64(const uint64_t *a, uint32_t n, uint64_t key) {
@@ -530,6 +581,13 @@ __device__ uint64_t *global_sort(uint64_t *g, uint64_t *h, uint32_t n, FmmLds &L
     return src;
 }
 
+// FMM loops handle kFB entries per thread per round (gather, claim, push,
+// the global-memory distance sweep)
+#ifndef OFD_FMM_B
+#define OFD_FMM_B 2
+#endif
+constexpr int kFB = OFD_FMM_B;
+
 // One fast march (icvCalcFMM / icvTeleaInpaintFMM's heap order) over the
 // pixels whose stamp is INF, starting from the band in log[0, nb).  Leaves
 // every push's stamp, distance and log entry; returns the number of log
@@ -564,33 +622,40 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
         }
         __syncthreads();
         uint32_t n = 0, tmn = INF, tmx = 0u;
-        for (uint32_t b = lo; b < hi; b += kThreads) {
-            const uint32_t i = b + tid;
-            float T = 0.f;
-            bool sel = false;
-            if (i < hi) {
-                T = m.logt[i];
-                sel = bucket_of(T) == k;
+        for (uint32_t b = lo; b < hi; b += kFB * kThreads) {  // 4 consecutive entries per thread: one load round
+            float T[kFB];
+            unsigned sel = 0;
+#pragma unroll
+            for (int u = 0; u < kFB; ++u) {
+                const uint32_t i = b + kFB * tid + u;
+                T[u] = i < hi ? m.logt[i] : 0.f;
+                if (i < hi && bucket_of(T[u]) == k) sel |= 1u << u;
             }
             uint32_t tot;
-            const uint32_t pos = block_scan(sel ? 1u : 0u, tot, L.scr);
-            if (sel) {
-                const uint32_t tb = __float_as_uint(T + 0.0f);  // -0 -> +0: the heap compares values
-                const uint64_t key = (uint64_t(tb) << 32) | i;
-                const uint32_t at = n + pos;
-                if (at < kCap)
-                    L.keys[at] = key;
-                else
-                    m.k0[at] = key;
-                tmn = min(tmn, tb);
-                tmx = max(tmx, tb);
-            }
+            uint32_t pos = block_scan(__popc(sel), tot, L.scr);
+#pragma unroll
+            for (int u = 0; u < kFB; ++u)
+                if (sel & (1u << u)) {
+                    const uint32_t i = b + kFB * tid + u;
+                    const uint32_t tb = __float_as_uint(T[u] + 0.0f);  // -0 -> +0: the heap compares values
+                    const uint64_t key = (uint64_t(tb) << 32) | i;
+                    const uint32_t at = n + pos++;
+                    if (at < kCap)
+                        L.keys[at] = key;
+                    else
+                        m.k0[at] = key;
+                    tmn = min(tmn, tb);
+                    tmx = max(tmx, tb);
+                }
             n += tot;
         }
         SQ_T(f1);
         SQ_ACC(0, f0, f1);
         if (n == 0) continue;
         ++nbuckets;
+#ifdef OFD_SQ_PROF
+        const int pb = n > uint32_t(kCap) ? 8 : 0;  // probe: large buckets in prof[8..]
+#endif
         if (tmn != INF) atomicMin(&L.tmin, tmn);
         atomicMax(&L.tmax, tmx);
         __syncthreads();
@@ -601,66 +666,75 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
             sync_all();
             keys = uniform ? m.k0 : (digit_sort(m.k0, m.k1, n, L) ? m.k1 : global_sort(m.k0, m.k1, n, L));
         } else if (!uniform && n > 1) {
-            if (n <= 512) {
-                // rank sort (unique keys): each key's place is the number of
-                // smaller keys -- broadcast LDS reads, no barrier per stage
-                for (uint32_t i = tid; i < n; i += kThreads) {
-                    const uint64_t key = L.keys[i];
-                    uint32_t r = 0;
-                    for (uint32_t j2 = 0; j2 < n; ++j2) r += L.keys[j2] < key ? 1u : 0u;
-                    L.keys[kCap / 2 + r] = key;
-                }
-                __syncthreads();
-                keys = L.keys + kCap / 2;
-            } else {
-                int mm = 1;
-                while (mm < int(n)) mm <<= 1;
-                for (int i = int(n) + tid; i < mm; i += kThreads) L.keys[i] = ~uint64_t(0);
-                __syncthreads();
-                lds_bitonic(L.keys, mm);
-            }
+            keys = lds_sort(L, n);
         }
         SQ_T(f2);
-        SQ_ACC(1, f1, f2);
+        SQ_ACC(pb + 1, f1, f2);
         // pops in order: claim the INSIDE neighbours (first claimant = pusher)
-        for (uint32_t r = tid; r < n; r += kThreads) {
-            const int64_t a = m.logp[uint32_t(keys[r])];
+        for (uint32_t r0 = tid; r0 < n; r0 += kFB * kThreads) {  // 4 pops per thread: one round per load step
+            int64_t a[kFB];
+            uint32_t sv[kFB][4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int64_t p = a + off[q];
-                if (st[p] == INF) atomicMin(&m.own[p], r * 4u + uint32_t(q));
+            for (int u = 0; u < kFB; ++u) {
+                const uint32_t r = r0 + uint32_t(u) * kThreads;
+                a[u] = r < n ? int64_t(m.logp[uint32_t(keys[r])]) : 0;
             }
+#pragma unroll
+            for (int u = 0; u < kFB; ++u)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) sv[u][q] = r0 + uint32_t(u) * kThreads < n ? st[a[u] + off[q]] : 0u;
+#pragma unroll
+            for (int u = 0; u < kFB; ++u)
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (sv[u][q] == INF)
+                        atomicMin(&m.own[a[u] + off[q]], (r0 + uint32_t(u) * kThreads) * 4u + uint32_t(q));
         }
         sync_all();
         SQ_T(f3);
-        SQ_ACC(2, f2, f3);
+        SQ_ACC(pb + 2, f2, f3);
         // pushes numbered in (rank, direction) order
         uint32_t npush = 0;
-        for (uint32_t b = 0; b < n; b += kThreads) {
-            const uint32_t r = b + tid;
-            int64_t a = 0;
-            unsigned mine = 0;
-            if (r < n) {
-                a = m.logp[uint32_t(keys[r])];
+        for (uint32_t b = 0; b < n; b += kFB * kThreads) {  // kFB slices of kThreads ranks, loads first
+            int64_t a[kFB];
+            uint32_t sv[kFB][4], ov[kFB][4];
 #pragma unroll
-                for (int q = 0; q < 4; ++q)  // a pixel pushed by an earlier bucket keeps a stale key
-                    if (st[a + off[q]] == INF && m.own[a + off[q]] == r * 4u + uint32_t(q)) mine |= 1u << q;
+            for (int u = 0; u < kFB; ++u) {
+                const uint32_t r = b + uint32_t(u) * kThreads + tid;
+                a[u] = r < n ? int64_t(m.logp[uint32_t(keys[r])]) : 0;
             }
-            uint32_t tot;
-            uint32_t pos = block_scan(__popc(mine), tot, L.scr);
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
-                if (mine & (1u << q)) {
-                    const uint32_t s = seq + npush + pos++;
-                    const int64_t p = a + off[q];
-                    st[p] = s;
-                    m.logp[s] = uint32_t(p);
+            for (int u = 0; u < kFB; ++u)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const bool in = b + uint32_t(u) * kThreads + tid < n;
+                    sv[u][q] = in ? st[a[u] + off[q]] : 0u;
+                    ov[u][q] = in ? m.own[a[u] + off[q]] : 0u;
                 }
-            npush += tot;
+#pragma unroll
+            for (int u = 0; u < kFB; ++u) {
+                if (b + uint32_t(u) * kThreads >= n) break;  // uniform
+                const uint32_t r = b + uint32_t(u) * kThreads + tid;
+                unsigned mine = 0;  // a pixel pushed by an earlier bucket keeps a stale key
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (sv[u][q] == INF && ov[u][q] == r * 4u + uint32_t(q)) mine |= 1u << q;
+                uint32_t tot;
+                uint32_t pos = block_scan(__popc(mine), tot, L.scr);
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (mine & (1u << q)) {
+                        const uint32_t s = seq + npush + pos++;
+                        const int64_t p = a[u] + off[q];
+                        st[p] = s;
+                        m.logp[s] = uint32_t(p);
+                    }
+                npush += tot;
+            }
         }
         sync_all();
         SQ_T(f4);
-        SQ_ACC(3, f3, f4);
+        SQ_ACC(pb + 3, f3, f4);
         // distances: sweep to the fixed point (acyclic in push order: at most
         // npush + 1 sweeps; the cap only guards against a broken invariant).
         // Up to kLdsPush pushes: the bucket's distances live in LDS and each
@@ -718,7 +792,7 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
                 const uint32_t c = L.chg;
                 __syncthreads();
 #ifdef OFD_SQ_PROF
-                if (tid == 0) prof[6] += 1;
+                if (tid == 0) prof[pb + 6] += 1;
 #endif
                 if (!c) break;
             }
@@ -728,46 +802,76 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
                 m.logt[seq + i] = T;
             }
             SQ_T(f5a);
-            SQ_ACC(4, f4, f5a);
+            SQ_ACC(pb + 4, f4, f5a);
             seq += npush;
             sync_all();
             SQ_T(f6a);
-            SQ_ACC(5, f5a, f6a);
-            if (n > uint32_t(kCap)) SQ_ACC(7, f1, f6a);
+            SQ_ACC(pb + 5, f5a, f6a);
             continue;
         }
-        for (uint32_t it = 0;; ++it) {
-            if (it > npush + 1) {
-                if (tid == 0) m.meta[5] = 2u;
-                break;
-            }
-            if (tid == 0) L.chg = 0u;
-            __syncthreads();
-            for (uint32_t i = tid; i < npush; i += kThreads) {
-                const uint32_t s = seq + i;
-                const int64_t p = m.logp[s];
-                const float T = fm_dist_seq(st, m.t, p, ew, s);
-                if (T != m.t[p]) {
-                    m.t[p] = T;
-                    L.chg = 1u;
+        // More pushes: sweep 0 evaluates every push; each later sweep only the
+        // pushes of this bucket next to one whose distance changed in the
+        // sweep before (a worklist, deduplicated by a per-sweep tag in own[]:
+        // claims are settled, and tags have the top bit, claims not).
+        {
+            uint32_t *wa = reinterpret_cast<uint32_t *>(m.k0), *wb = reinterpret_cast<uint32_t *>(m.k1);
+            uint32_t nw = npush;
+            for (uint32_t it = 0;; ++it) {
+                if (it > npush + 1) {
+                    if (tid == 0) m.meta[5] = 2u;
+                    break;
                 }
-            }
-            sync_all();
-            const uint32_t c = L.chg;
-            __syncthreads();
+                if (tid == 0) L.chg = 0u;
+                __syncthreads();
+                const uint32_t tag = 0x80000000u | it;
+                for (uint32_t i0 = tid; i0 < nw; i0 += kFB * kThreads) {
+                    int64_t p[kFB];
+                    uint32_t sp[kFB];
+                    float T[kFB], cur[kFB];
+#pragma unroll
+                    for (int u = 0; u < kFB; ++u) {
+                        const uint32_t i = i0 + uint32_t(u) * kThreads;
+                        const uint32_t x = i < nw ? (it == 0 ? i : wa[i]) : 0u;
+                        sp[u] = seq + x;
+                        p[u] = i < nw ? int64_t(m.logp[seq + x]) : int64_t(ew) + 1;
+                    }
+#pragma unroll
+                    for (int u = 0; u < kFB; ++u) {
+                        T[u] = fm_dist_seq(st, m.t, p[u], ew, sp[u]);
+                        cur[u] = m.t[p[u]];
+                    }
+#pragma unroll
+                    for (int u = 0; u < kFB; ++u)
+                        if (i0 + uint32_t(u) * kThreads < nw && T[u] != cur[u]) {
+                            m.t[p[u]] = T[u];
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) {
+                                const int64_t nq = p[u] + off[q];
+                                const uint32_t sn = st[nq];
+                                if (sn > sp[u] && sn != INF && atomicExch(&m.own[nq], tag) != tag)
+                                    wb[atomicAdd(&L.chg, 1u)] = sn - seq;
+                            }
+                        }
+                }
+                sync_all();
+                nw = L.chg;
+                __syncthreads();
 #ifdef OFD_SQ_PROF
-            if (tid == 0) prof[6] += 1;
+                if (tid == 0) prof[pb + 6] += 1;
 #endif
-            if (!c) break;
+                uint32_t *tmp = wa;
+                wa = wb;
+                wb = tmp;
+                if (nw == 0) break;
+            }
         }
         SQ_T(f5);
-        SQ_ACC(4, f4, f5);
+        SQ_ACC(pb + 4, f4, f5);
         for (uint32_t i = tid; i < npush; i += kThreads) m.logt[seq + i] = m.t[m.logp[seq + i]];
         seq += npush;
         sync_all();
         SQ_T(f6);
-        SQ_ACC(5, f5, f6);
-        SQ_ACC(7, f1, f6);  // buckets past the LDS capacities
+        SQ_ACC(pb + 5, f5, f6);
     }
     return seq;
 }
@@ -778,7 +882,7 @@ __global__ __launch_bounds__(kThreads) void sq_fmm_kernel(SqWs w) {
     const uint32_t nb = m.meta[0];
     uint32_t nbo = 0, nbi = 0;
     // outer march over the ring (icvCalcFMM(out, t, Out, negate = true))
-    uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t prof[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     const uint32_t no = fmm_pass(m, m.sO, nb, L, nbo, prof);
     for (uint32_t i = threadIdx.x; i < no; i += kThreads) {
         const uint32_t p = m.logp[i];
@@ -792,6 +896,9 @@ __global__ __launch_bounds__(kThreads) void sq_fmm_kernel(SqWs w) {
         m.meta[2] = 0u;
         m.meta[4] = nbo + nbi;
         for (int k = 0; k < 8; ++k) m.meta[8 + k] = uint32_t(k == 6 ? prof[k] : prof[k] >> 8);
+#ifdef OFD_SQ_PROF
+        for (int k = 0; k < 8; ++k) m.meta[24 + k] = uint32_t(k == 6 ? prof[8 + k] : prof[8 + k] >> 8);
+#endif
     }
 }
 

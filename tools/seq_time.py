@@ -60,7 +60,9 @@ def main():
         if m[:, 8:24].any():
             r = m[kdeep]
             print("FMM   gather/sort/claim/push/dist/log (Mclk):", [round(x * 256 / 1e6, 2) for x in r[8:14]],
-                  "sweeps", int(r[14]), "big buckets (sort..log)", round(r[15] * 256 / 1e6, 2))
+                  "sweeps", int(r[14]))
+            print("FMM (buckets > 4096 keys) -/sort/claim/push/dist/log (Mclk):",
+                  [round(x * 256 / 1e6, 2) for x in r[24:30]], "sweeps", int(r[30]))
             print("COLOUR3 level work/barrier, per-round loads/terms/chains/final+append/atomics (Mclk):",
                   [round(x * 256 / 1e6, 2) for x in r[16:23]])
         print("max levels", m[:, 3].max(), "max buckets", m[:, 4].max(), "errors", int((m[:, 5] != 0).sum()))
