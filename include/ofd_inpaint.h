@@ -66,8 +66,11 @@ int ofd_inpaint_telea_f32(const float *img, const float *valid, const float *col
                           size_t workspace_bytes, void *stream);
 
 /* Bytes of workspace for ofd_inpaint_telea_seq_f32 over B images of H x W
- * (about 40 bytes per padded pixel; any size of at least one image's share
- * works, larger ones process more images per launch). */
+ * (about 212 bytes per padded pixel: stamps, distances, push log and sort
+ * buffers, 160-byte per-hole colour records and the packed colour image of
+ * the radius-3 path; any size of at least one image's share works, larger
+ * ones process more images per launch -- the fill is latency-bound per
+ * image, so a whole batch per launch is the fast choice on 288 GB). */
 size_t ofd_inpaint_seq_workspace_bytes(int64_t B, int64_t H, int64_t W);
 
 /* utils.inpaint, batched, in cv2's exact order: the same arguments and
