@@ -1582,6 +1582,82 @@ int run_f32(Coords co, const E *obj, const float *depth, E *out, float *valid, f
 
 }  // namespace
 
+namespace {
+// Disparity warps (preprocess.py:356-359) move every source along its own
+// row: the flow is (-s*50/d, -0), and fw.py's clamp keeps y + -0 = y.  So the
+// fused disparity warp needs no BIN and no tile lists: one workgroup per
+// image row folds the row's keys into an LDS z-buffer (ds_min_u64 on the
+// same lexmin key as every engine) and publishes the row -- the winners' obj
+// channels (same row: L1 / L2 hits), the generated depth / disparity / +0
+// channels, valid and collision.  Bit-identical to the tile engine on the
+// same call (tests/test_fused.py); 48 B/px of HBM traffic at C = 6.
+constexpr int kRowThr = 256;
+constexpr int kRowMaxW = 8192;  // 64 KB of keys per workgroup
+
+template <typename D>
+__global__ __launch_bounds__(kRowThr) void disp_row_kernel(DisparityCoords<D> co, const float *__restrict__ obj,
+                                                         float *__restrict__ out, float *__restrict__ valid,
+                                                         float *__restrict__ coll, int Cobj, int gen_at, int H, int W) {
+    extern __shared__ unsigned long long zrow[];
+    const int64_t row = blockIdx.x;
+    const int64_t b = row / H;
+    const int j = int(row - b * H);
+    const int64_t HW = int64_t(H) * W;
+    for (int x = threadIdx.x; x < W; x += kRowThr) zrow[x] = KEY_UNTOUCHED;
+    __syncthreads();
+    const D *dr = co.depth + b * HW + int64_t(j) * W;
+    for (int x = threadIdx.x; x < W; x += kRowThr) {
+        const D d = dr[x];
+        int tx, ty;
+        target_flow<D>(x, j, -co.disp(b, d), -D(0), H, W, tx, ty);
+        if (tx >= 0) atomicMin(&zrow[tx], make_key(float(d), unsigned(j * W + x)));
+    }
+    __syncthreads();
+    const int C = Cobj + 3;
+    const float *ob = obj + b * int64_t(Cobj) * HW;
+    float *oo = out + b * int64_t(C) * HW;
+    const unsigned uHW = unsigned(HW);
+    for (int x = threadIdx.x; x < W; x += kRowThr) {
+        const unsigned long long key = zrow[x];
+        const bool touched = key != KEY_UNTOUCHED, nowin = key == KEY_NOWIN;
+        const unsigned t = unsigned(j) * unsigned(W) + unsigned(x);
+        const unsigned w = (touched && !nowin) ? unsigned(key & 0xFFFFFFFFull) : WIN_NONE;
+        __builtin_nontemporal_store(touched ? 1.f : 0.f, valid + b * HW + t);
+        __builtin_nontemporal_store(nowin ? 1.f : 0.f, coll + b * HW + t);
+        float g[3] = {0.f, 0.f, 0.f};
+        if (w != WIN_NONE) co.gen_key(b, w, key, g);
+        for (int c = 0; c < Cobj; ++c) {
+            const float v = w != WIN_NONE ? ob[unsigned(c) * uHW + w] : 0.f;
+            __builtin_nontemporal_store(v, oo + unsigned(c < gen_at ? c : c + 3) * uHW + t);
+        }
+#pragma unroll
+        for (int e = 0; e < 3; ++e) __builtin_nontemporal_store(g[e], oo + unsigned(gen_at + e) * uHW + t);
+    }
+}
+
+bool disp_row_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("OFD_DISP_ROW");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+template <typename D>
+int warp_disparity_rows(DisparityCoords<D> co, const float *obj, int64_t Cobj, float *output, float *valid,
+                        float *collision, int64_t B, int64_t H, int64_t W, hipStream_t st) {
+    const int gen_at = int(Cobj < 3 ? Cobj : 3);
+    hipLaunchKernelGGL(disp_row_kernel<D>, dim3(unsigned(B * H)), dim3(kRowThr), size_t(W) * 8, st, co, obj, output,
+                       valid, collision, int(Cobj), gen_at, int(H), int(W));
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? OFD_FW_OK : int(e);
+}
+
+bool rows_ok(int64_t B, int64_t C, int64_t H, int64_t W) {
+    return disp_row_enabled() && W <= kRowMaxW && C * H * W < (int64_t(1) << 31) && B * H < (int64_t(1) << 31);
+}
+}  // namespace
+
 extern "C" {
 
 int ofd_fw_abi_version(void) { return OFD_FW_ABI_VERSION; }
@@ -1688,6 +1764,8 @@ int ofd_fw_warp_disparity_f32(const float *obj, int64_t Cobj, const float *depth
     if (B * H * W > 0 && (!depth || !s || !valid || !collision || !output || (Cobj > 0 && !obj)))
         return OFD_FW_EINVAL;
     DisparityCoords<float> co{depth, s, H * W};
+    if (B * H * W > 0 && rows_ok(B, C, H, W))
+        return warp_disparity_rows(co, obj, Cobj, output, valid, collision, B, H, W, static_cast<hipStream_t>(stream));
     return run_f32(co, obj, nullptr, output, valid, collision, B, C, H, W, workspace, workspace_bytes,
                    static_cast<hipStream_t>(stream), int(Cobj < 3 ? Cobj : 3));
 }
@@ -1702,6 +1780,8 @@ int ofd_fw_warp_disparity_f64depth(const float *obj, int64_t Cobj, const double 
         return OFD_FW_EINVAL;
     if (!aligned(depth, 8)) return OFD_FW_EALIGN;
     DisparityCoords<double> co{depth, s, H * W};
+    if (B * H * W > 0 && rows_ok(B, C, H, W))
+        return warp_disparity_rows(co, obj, Cobj, output, valid, collision, B, H, W, static_cast<hipStream_t>(stream));
     return run_f32(co, obj, nullptr, output, valid, collision, B, C, H, W, workspace, workspace_bytes,
                    static_cast<hipStream_t>(stream), int(Cobj < 3 ? Cobj : 3));
 }
