@@ -1592,9 +1592,10 @@ namespace {
 // channels, valid and collision.  Bit-identical to the tile engine on the
 // same call (tests/test_fused.py); 48 B/px of HBM traffic at C = 6.
 constexpr int kRowThr = 256;
+typedef float RowF4 __attribute__((ext_vector_type(4)));
 constexpr int kRowMaxW = 8192;  // 64 KB of keys per workgroup
 
-template <typename D>
+template <typename D, bool kVec>
 __global__ __launch_bounds__(kRowThr) void disp_row_kernel(DisparityCoords<D> co, const float *__restrict__ obj,
                                                          float *__restrict__ out, float *__restrict__ valid,
                                                          float *__restrict__ coll, int Cobj, int gen_at, int H, int W) {
@@ -1606,32 +1607,64 @@ __global__ __launch_bounds__(kRowThr) void disp_row_kernel(DisparityCoords<D> co
     for (int x = threadIdx.x; x < W; x += kRowThr) zrow[x] = KEY_UNTOUCHED;
     __syncthreads();
     const D *dr = co.depth + b * HW + int64_t(j) * W;
-    for (int x = threadIdx.x; x < W; x += kRowThr) {
-        const D d = dr[x];
-        int tx, ty;
-        target_flow<D>(x, j, -co.disp(b, d), -D(0), H, W, tx, ty);
-        if (tx >= 0) atomicMin(&zrow[tx], make_key(float(d), unsigned(j * W + x)));
+    // kVec (W % 4 == 0, 16-byte aligned planes): four consecutive pixels per
+    // thread, 16-byte loads and stores
+    constexpr int kP = kVec ? 4 : 1;
+    for (int x0 = kP * threadIdx.x; x0 < W; x0 += kP * kRowThr) {
+        D d[kP];
+        if constexpr (kVec)
+            ::load4<true>(dr + x0, d, 4);
+        else
+            d[0] = dr[x0];
+#pragma unroll
+        for (int e = 0; e < kP; ++e) {
+            int tx, ty;
+            target_flow<D>(x0 + e, j, -co.disp(b, d[e]), -D(0), H, W, tx, ty);
+            if (tx >= 0) atomicMin(&zrow[tx], make_key(float(d[e]), unsigned(j * W + x0 + e)));
+        }
     }
     __syncthreads();
     const int C = Cobj + 3;
     const float *ob = obj + b * int64_t(Cobj) * HW;
     float *oo = out + b * int64_t(C) * HW;
     const unsigned uHW = unsigned(HW);
-    for (int x = threadIdx.x; x < W; x += kRowThr) {
-        const unsigned long long key = zrow[x];
-        const bool touched = key != KEY_UNTOUCHED, nowin = key == KEY_NOWIN;
-        const unsigned t = unsigned(j) * unsigned(W) + unsigned(x);
-        const unsigned w = (touched && !nowin) ? unsigned(key & 0xFFFFFFFFull) : WIN_NONE;
-        __builtin_nontemporal_store(touched ? 1.f : 0.f, valid + b * HW + t);
-        __builtin_nontemporal_store(nowin ? 1.f : 0.f, coll + b * HW + t);
-        float g[3] = {0.f, 0.f, 0.f};
-        if (w != WIN_NONE) co.gen_key(b, w, key, g);
+    auto put = [&](float *dst, const float v[kP]) {
+        if constexpr (kVec)
+            __builtin_nontemporal_store(RowF4{v[0], v[1], v[2], v[3]}, reinterpret_cast<RowF4 *>(dst));
+        else
+            __builtin_nontemporal_store(v[0], dst);
+    };
+    for (int x0 = kP * threadIdx.x; x0 < W; x0 += kP * kRowThr) {
+        unsigned long long key[kP];
+        unsigned w[kP];
+        float vv[kP], cv[kP];
+#pragma unroll
+        for (int e = 0; e < kP; ++e) {
+            key[e] = zrow[x0 + e];
+            const bool touched = key[e] != KEY_UNTOUCHED, nowin = key[e] == KEY_NOWIN;
+            w[e] = (touched && !nowin) ? unsigned(key[e] & 0xFFFFFFFFull) : WIN_NONE;
+            vv[e] = touched ? 1.f : 0.f;
+            cv[e] = nowin ? 1.f : 0.f;
+        }
+        const unsigned t = unsigned(j) * unsigned(W) + unsigned(x0);
+        put(valid + b * HW + t, vv);
+        put(coll + b * HW + t, cv);
         for (int c = 0; c < Cobj; ++c) {
-            const float v = w != WIN_NONE ? ob[unsigned(c) * uHW + w] : 0.f;
-            __builtin_nontemporal_store(v, oo + unsigned(c < gen_at ? c : c + 3) * uHW + t);
+            float v[kP];
+#pragma unroll
+            for (int e = 0; e < kP; ++e) v[e] = w[e] != WIN_NONE ? ob[unsigned(c) * uHW + w[e]] : 0.f;
+            put(oo + unsigned(c < gen_at ? c : c + 3) * uHW + t, v);
+        }
+        float g[3][kP];
+#pragma unroll
+        for (int e = 0; e < kP; ++e) {
+            float ge[3] = {0.f, 0.f, 0.f};
+            if (w[e] != WIN_NONE) co.gen_key(b, w[e], key[e], ge);
+#pragma unroll
+            for (int q = 0; q < 3; ++q) g[q][e] = ge[q];
         }
 #pragma unroll
-        for (int e = 0; e < 3; ++e) __builtin_nontemporal_store(g[e], oo + unsigned(gen_at + e) * uHW + t);
+        for (int q = 0; q < 3; ++q) put(oo + unsigned(gen_at + q) * uHW + t, g[q]);
     }
 }
 
@@ -1647,8 +1680,14 @@ template <typename D>
 int warp_disparity_rows(DisparityCoords<D> co, const float *obj, int64_t Cobj, float *output, float *valid,
                         float *collision, int64_t B, int64_t H, int64_t W, hipStream_t st) {
     const int gen_at = int(Cobj < 3 ? Cobj : 3);
-    hipLaunchKernelGGL(disp_row_kernel<D>, dim3(unsigned(B * H)), dim3(kRowThr), size_t(W) * 8, st, co, obj, output,
-                       valid, collision, int(Cobj), gen_at, int(H), int(W));
+    const bool vec = W % 4 == 0 && aligned(co.depth, 16) && aligned(output, 16) && aligned(valid, 16) &&
+                     aligned(collision, 16);
+    if (vec)
+        hipLaunchKernelGGL((disp_row_kernel<D, true>), dim3(unsigned(B * H)), dim3(kRowThr), size_t(W) * 8, st, co, obj,
+                           output, valid, collision, int(Cobj), gen_at, int(H), int(W));
+    else
+        hipLaunchKernelGGL((disp_row_kernel<D, false>), dim3(unsigned(B * H)), dim3(kRowThr), size_t(W) * 8, st, co,
+                           obj, output, valid, collision, int(Cobj), gen_at, int(H), int(W));
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? OFD_FW_OK : int(e);
 }
