@@ -85,3 +85,32 @@ def test_warp_disparity_headline_batch():
     exp = forward_warp_flow(obj.to(dev), flow.to(dev), d.to(dev).to(torch.float32))
     for g_, e_ in zip(got, exp):
         assert torch.equal(g_, e_)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+@pytest.mark.parametrize("W", [64, 53])
+def test_warp_disparity_special_depths(dtype, W):
+    """The row kernel (one workgroup per image row, 16-byte and scalar lanes)
+    on depths the reference's z-test treats specially: 0 (infinite disparity,
+    clamped onto column 0), NaN (dropped), >= 1000 (lands, never wins: a
+    collision), negative and -0.0 (win), and runs of equal depths (ties go to
+    the first source in raster order)."""
+    from opticalflowfromdepth_amd import forward_warp_flow, warp_disparity
+    B, H = 2, 12
+    rgb, d, s, ex = _inputs(B, H, W, dtype, 77, 1)
+    g = torch.Generator().manual_seed(3)
+    pick = torch.rand(B, 1, H, W, generator=g)
+    specials = torch.tensor([0.0, float("nan"), 1000.0, 2500.0, -1.5, -0.0, 0.25], dtype=dtype)
+    idx = torch.randint(0, len(specials), (B, 1, H, W), generator=g)
+    d = torch.where(pick < 0.25, specials[idx], d)
+    d[:, :, 3, 10:30] = d[:, :, 3, 10:11]  # a run of equal depths: many sources tie on few targets
+    obj, flow = _unfused(rgb, d, s, ex)
+    dev = torch.device("cuda:0")
+    got = warp_disparity(torch.cat((rgb, ex), 1).to(dev), d.to(dev), s)
+    exp_gpu = forward_warp_flow(obj.to(dev), flow.to(dev), d.to(dev).to(torch.float32))
+    exp_cpu = oracle.fw_flow(obj.numpy(), flow.numpy(), d.to(torch.float32).numpy())
+    for g_, e_, c_, n in zip(got, exp_gpu, exp_cpu, ("output", "valid", "collision")):
+        g_ = g_.cpu().numpy()
+        assert np.array_equal(g_, e_.cpu().numpy(), equal_nan=True), n
+        assert np.array_equal(g_, c_, equal_nan=True), n
