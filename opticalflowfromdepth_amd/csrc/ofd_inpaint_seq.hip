@@ -320,6 +320,8 @@ __global__ __launch_bounds__(256) void sq_band_write_kernel(SqWs w) {
             const uint32_t s = off + __popcll(bal & ((uint64_t(1) << lane) - 1));
             m.logp[s] = uint32_t(p);
             m.logt[s] = 0.f;
+            m.rec[s] = uint32_t(p);  // the outer march's log (outer_view)
+            reinterpret_cast<float *>(m.rec + m.en)[s] = 0.f;
         }
         off += __popcll(bal);
     }
@@ -345,10 +347,21 @@ __device__ __forceinline__ uint32_t bucket_of(float T) { return uint32_t(T * 2.0
 // distance of padded pixel p pushed with seq s: FastMarching_solve over the
 // neighbours reached before it (stamp < s); cv2's fm order (up/left,
 // down/left, up/right, down/right)
+// The inner march runs beside the outer one (sq_fmm_kernel), whose final
+// negation turns the band's distances from +0 to -0 at some point during it;
+// the inner march reads a band distance as the -0 it would see after the
+// outer march (the only pixels with a zero distance are band pixels).
+template <bool kInner>
+__device__ __forceinline__ float band_t(float v) {
+    return (kInner && v == 0.f) ? -0.f : v;
+}
+
+template <bool kInner>
 __device__ __forceinline__ float fm_dist_seq(const uint32_t *st, const float *t, int64_t p, int ew, uint32_t s) {
     const int64_t nu = p - ew, nd = p + ew, nl = p - 1, nr = p + 1;
     const bool iu = st[nu] >= s, id = st[nd] >= s, il = st[nl] >= s, ir = st[nr] >= s;
-    const float tu = iu ? T_FAR : t[nu], td = id ? T_FAR : t[nd], tl = il ? T_FAR : t[nl], tr = ir ? T_FAR : t[nr];
+    const float tu = iu ? T_FAR : band_t<kInner>(t[nu]), td = id ? T_FAR : band_t<kInner>(t[nd]),
+                tl = il ? T_FAR : band_t<kInner>(t[nl]), tr = ir ? T_FAR : band_t<kInner>(t[nr]);
     return min4f(fm_solve(tu, iu, tl, il), fm_solve(td, id, tl, il), fm_solve(tu, iu, tr, ir),
                  fm_solve(td, id, tr, ir));
 }
@@ -592,6 +605,7 @@ constexpr int kFB = OFD_FMM_B;
 // pixels whose stamp is INF, starting from the band in log[0, nb).  Leaves
 // every push's stamp, distance and log entry; returns the number of log
 // entries (band + pushes).
+template <bool kInner>
 __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L, uint32_t &nbuckets, uint64_t *prof) {
     (void)prof;
     const int tid = threadIdx.x, ew = m.ew;
@@ -755,7 +769,7 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
                         const int64_t nq = p + off[q];
                         const uint32_t sn = st[nq];
                         lk[u][q] = sn >= sp ? -2 : (sn >= seq ? int(sn - seq) : -1);
-                        fv[u][q] = lk[u][q] == -1 ? m.t[nq] : T_FAR;
+                        fv[u][q] = lk[u][q] == -1 ? band_t<kInner>(m.t[nq]) : T_FAR;
                     }
                     Tl[i] = T_FAR;
                 }
@@ -837,7 +851,7 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
                     }
 #pragma unroll
                     for (int u = 0; u < kFB; ++u) {
-                        T[u] = fm_dist_seq(st, m.t, p[u], ew, sp[u]);
+                        T[u] = fm_dist_seq<kInner>(st, m.t, p[u], ew, sp[u]);
                         cur[u] = m.t[p[u]];
                     }
 #pragma unroll
@@ -876,25 +890,44 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
     return seq;
 }
 
+// The outer march's push log and sort buffers: the record area, which is
+// free until RECORD (24 of its 160 bytes per padded pixel).
+__device__ __forceinline__ Img outer_view(const Img &m) {
+    Img o = m;
+    o.logp = m.rec;
+    o.logt = reinterpret_cast<float *>(m.rec + m.en);
+    o.k0 = reinterpret_cast<uint64_t *>(m.rec + 2 * m.en);
+    o.k1 = o.k0 + m.en;
+    return o;
+}
+
+// Two workgroups per image: blockIdx.y = 0 runs the outer march over the ring
+// (icvCalcFMM(out, t, Out, negate = true)) and negates its distances,
+// blockIdx.y = 1 the inner march over the holes (icvTeleaInpaintFMM's order).
+// They touch disjoint pixels (ring pixels are not 4-adjacent to holes) and
+// keep separate stamps, logs and sort buffers; the only value both read is
+// the band's zero distance (band_t).
 __global__ __launch_bounds__(kThreads) void sq_fmm_kernel(SqWs w) {
     __shared__ FmmLds L;
     const Img m = image(w, blockIdx.x);
     const uint32_t nb = m.meta[0];
-    uint32_t nbo = 0, nbi = 0;
-    // outer march over the ring (icvCalcFMM(out, t, Out, negate = true))
+    uint32_t nbk = 0;
     uint64_t prof[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    const uint32_t no = fmm_pass(m, m.sO, nb, L, nbo, prof);
-    for (uint32_t i = threadIdx.x; i < no; i += kThreads) {
-        const uint32_t p = m.logp[i];
-        m.t[p] = -m.t[p];
+    if (blockIdx.y == 0) {
+        const Img o = outer_view(m);
+        const uint32_t no = fmm_pass<false>(o, m.sO, nb, L, nbk, prof);
+        for (uint32_t i = threadIdx.x; i < no; i += kThreads) {
+            const uint32_t p = o.logp[i];
+            m.t[p] = -m.t[p];
+        }
+        if (threadIdx.x == 0) atomicAdd(&m.meta[4], nbk);
+        return;
     }
-    sync_all();
-    // inner march over the holes (icvTeleaInpaintFMM's order)
-    const uint32_t ni = fmm_pass(m, m.sI, nb, L, nbi, prof);
+    const uint32_t ni = fmm_pass<true>(m, m.sI, nb, L, nbk, prof);
     if (threadIdx.x == 0) {
         m.meta[1] = ni - nb;
         m.meta[2] = 0u;
-        m.meta[4] = nbo + nbi;
+        atomicAdd(&m.meta[4], nbk);
         for (int k = 0; k < 8; ++k) m.meta[8 + k] = uint32_t(k == 6 ? prof[k] : prof[k] >> 8);
 #ifdef OFD_SQ_PROF
         for (int k = 0; k < 8; ++k) m.meta[24 + k] = uint32_t(k == 6 ? prof[8 + k] : prof[8 + k] >> 8);
@@ -1702,7 +1735,7 @@ int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float 
         hipLaunchKernelGGL(sq_init_kernel, dim3(unsigned((w.eh + 3) / 4), unsigned(nb)), dim3(256), 0, st, w, r);
         hipLaunchKernelGGL(sq_band_scan_kernel, dim3(unsigned(nb)), dim3(kThreads), 0, st, w);
         hipLaunchKernelGGL(sq_band_write_kernel, dim3(unsigned((w.eh + 3) / 4), unsigned(nb)), dim3(256), 0, st, w);
-        hipLaunchKernelGGL(sq_fmm_kernel, dim3(unsigned(nb)), dim3(kThreads), 0, st, w);
+        hipLaunchKernelGGL(sq_fmm_kernel, dim3(unsigned(nb), 2u), dim3(kThreads), 0, st, w);
         if (rec3) {
             hipLaunchKernelGGL(sq_record3_kernel, dim3(unsigned((w.ew + 63) / 64), unsigned((w.eh + 3) / 4), unsigned(nb)),
                                dim3(256), 0, st, w);
