@@ -1614,18 +1614,21 @@ __global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, int C, int H, 
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             SQ_T(c2);
-            // cv2's sums in its (k, l) order, one chain per lane
-            for (int cn = gl; cn < nch; cn += kL3) {
-                const float *tc = bf + cn * kDisk;
-                float acc = 0.f;
-                if (cn % 3 == 0) {
+            // cv2's sums in its (k, l) order: chains gl and gl + 8 side by side
+            // (independent accumulators; Ia chains add, Jx / Jy chains subtract)
+            {
+                const int c1 = gl, c2 = gl + kL3;
+                const bool has2 = c2 < nch;
+                const float *t1 = bf + c1 * kDisk, *t2 = bf + (has2 ? c2 : c1) * kDisk;
+                const float s1 = c1 % 3 == 0 ? 1.f : -1.f, s2 = c2 % 3 == 0 ? 1.f : -1.f;
+                float a1 = 0.f, a2 = 0.f;
 #pragma unroll
-                    for (int q = 0; q < kDisk; ++q) acc += tc[q];
-                } else {
-#pragma unroll
-                    for (int q = 0; q < kDisk; ++q) acc -= tc[q];
+                for (int q = 0; q < kDisk; ++q) {
+                    a1 += s1 * t1[q];  // x * +-1 is exact: acc + (-t) == acc - t
+                    a2 += s2 * t2[q];
                 }
-                L.res[g][cn] = acc;
+                if (c1 < nch) L.res[g][c1] = a1;
+                if (has2) L.res[g][c2] = a2;
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
