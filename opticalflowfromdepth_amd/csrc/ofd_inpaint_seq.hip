@@ -1386,17 +1386,33 @@ __device__ __forceinline__ void val_pos(int e, int &a, int &b) {
 // mask over win_pos order; word 38 = cv2's weight sum).  Also the Kahn
 // counter (record index << 6 | earlier holes in the window) and level 0.
 __global__ __launch_bounds__(256) void sq_record3_kernel(SqWs w) {
+    // The workgroup's 64 x 4 pixels with a 4-pixel halo (clamped to the
+    // padded image) of stamps and distances in LDS: every window read below
+    // is an LDS read.
+    constexpr int TR = 4 + 8, TC = 64 + 8;
+    __shared__ uint32_t Ls[TR][TC];
+    __shared__ float Lt[TR][TC];
     const int j = blockIdx.x * 64 + (threadIdx.x & 63), i = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const int i0 = int(blockIdx.y) * 4 - 4, j0 = int(blockIdx.x) * 64 - 4;
     const Img m = image(w, blockIdx.z);
     const int eh = m.eh, ew = m.ew;
+    for (int e = threadIdx.x; e < TR * TC; e += 256) {
+        const int r = e / TC, c = e - r * TC;
+        const int64_t q = int64_t(min(max(i0 + r, 0), eh - 1)) * ew + min(max(j0 + c, 0), ew - 1);
+        Ls[r][c] = m.sI[q];
+        Lt[r][c] = m.t[q];
+    }
+    __syncthreads();
     if (i < 1 || j < 1 || i >= eh - 1 || j >= ew - 1) return;
     const int64_t p = int64_t(i) * ew + j;
-    const uint32_t *st = m.sI;
-    const uint32_t s = st[p];
+    const int li = i - i0, lj = j - j0;
+    auto S = [&](int y, int x) -> uint32_t { return Ls[y - i0][x - j0]; };   // |y - i|, |x - j| <= 4
+    auto TT = [&](int y, int x) -> float { return Lt[y - i0][x - j0]; };
+    const uint32_t s = Ls[li][lj];
     if (s == 0u || s == INF) return;
     const uint32_t idx = s - m.meta[0];
-    auto at = [&](int y, int x) -> int64_t { return int64_t(min(max(y, 0), eh - 1)) * ew + min(max(x, 0), ew - 1); };
-    // Kahn counter and dependants: window positions inside the image
+    // Kahn counter and dependants: window positions inside the image (the
+    // tile's clamped halo holds the image's own pixels there)
     uint32_t cnt = 0;
     uint64_t dep = 0;
     int bit = 0;
@@ -1407,15 +1423,15 @@ __global__ __launch_bounds__(256) void sq_record3_kernel(SqWs w) {
             if (!win3(a, b) || !(a || b)) continue;
             const int y = i + a, x = j + b;
             if (y >= 1 && x >= 1 && y < eh - 1 && x < ew - 1) {
-                const uint32_t q = st[int64_t(y) * ew + x];
+                const uint32_t q = S(y, x);
                 cnt += (q != 0u && q < s) ? 1u : 0u;
                 if (q > s && q != INF) dep |= uint64_t(1) << bit;
             }
             ++bit;
         }
     // cv2's distance gradient at the hole
-    const uint32_t su = st[p - ew], sd = st[p + ew], sl = st[p - 1], sr = st[p + 1];
-    const float tij = m.t[p], tu = m.t[p - ew], td = m.t[p + ew], tl = m.t[p - 1], tr = m.t[p + 1];
+    const uint32_t su = S(i - 1, j), sd = S(i + 1, j), sl = S(i, j - 1), sr = S(i, j + 1);
+    const float tij = TT(i, j), tu = TT(i - 1, j), td = TT(i + 1, j), tl = TT(i, j - 1), tr = TT(i, j + 1);
     float gtx, gty;
     if (!(sr >= s))
         gtx = !(sl >= s) ? (tr - tl) * 0.5f : (tr - tij);
@@ -1437,17 +1453,17 @@ __global__ __launch_bounds__(256) void sq_record3_kernel(SqWs w) {
             if (!disk3(a, b)) continue;
             const int y = i + a, x = j + b;
             const bool inimg = y > 0 && x > 0 && y < eh - 1 && x < ew - 1;
-            const bool used = inimg && !(st[at(y, x)] >= s);
+            const bool used = inimg && !(S(y, x) >= s);
             const float ry = float(-a), rx = float(-b);
             const float len2 = rx * rx + ry * ry;
             const float dst = float(1. / (double(len2) * sqrt(double(len2))));
-            const float lev = float(1. / (1 + fabs(double(m.t[at(y, x)] - tij))));
+            const float lev = float(1. / (1 + fabs(double(TT(y, x) - tij))));
             float dir = rx * gtx + ry * gty;
             if (fabs(double(dir)) <= 0.01) dir = 0.000001f;
             const float wt = used ? float(fabs(double(dst * lev * dir))) : 0.f;
             sum += wt;
-            const bool nr = !(st[at(y, x + 1)] >= s), nl = !(st[at(y, x - 1)] >= s);
-            const bool nd = !(st[at(y + 1, x)] >= s), nu = !(st[at(y - 1, x)] >= s);
+            const bool nr = !(S(y, x + 1) >= s), nl = !(S(y, x - 1) >= s);
+            const bool nd = !(S(y + 1, x) >= s), nu = !(S(y - 1, x) >= s);
             const uint32_t cx = nr ? (nl ? 0u : 1u) : (nl ? 2u : 3u);
             const uint32_t cy = nd ? (nu ? 0u : 1u) : (nu ? 2u : 3u);
             const int l = d % kL3, k = d / kL3;
