@@ -86,6 +86,14 @@ int ofd_fw_abi_version(void);
 #define OFD_FW_ENGINE_TILE_SPLIT 2
 int ofd_fw_set_engine(int engine);
 
+/* The fused disparity warps (ofd_fw_warp_disparity_*) move every source
+ * along its own row, and by default run on a row kernel (one workgroup per
+ * image row, LDS z-buffer; rows up to 8192 wide) instead of the TILE engine;
+ * results are identical.  on = 1 / 0 selects the row kernel / the TILE
+ * engine for subsequent calls (also OFD_DISP_ROW=0); any other value only
+ * queries.  Returns the previous setting.  Process-wide, not thread-safe. */
+int ofd_fw_set_disparity_rows(int on);
+
 /* Benchmark hook: when non-NULL, the given hipEvent_t's are recorded on the
  * launch stream right before the first and right after the last launch of
  * each subsequent f32 call's dominant kernel: SPLAT (TILE engine), RESOLVE

@@ -1668,12 +1668,14 @@ __global__ __launch_bounds__(kRowThr) void disp_row_kernel(DisparityCoords<D> co
     }
 }
 
+int g_disp_rows = -1;  // ofd_fw_set_disparity_rows; -1: OFD_DISP_ROW (default on)
+
 bool disp_row_enabled() {
-    static const bool on = [] {
+    static const bool env_on = [] {
         const char *e = getenv("OFD_DISP_ROW");
         return !(e && e[0] == '0');
     }();
-    return on;
+    return g_disp_rows < 0 ? env_on : g_disp_rows != 0;
 }
 
 template <typename D>
@@ -1705,6 +1707,12 @@ int ofd_fw_set_profile_events(void *start_event, void *stop_event) {
     g_prof_start = static_cast<hipEvent_t>(start_event);
     g_prof_stop = static_cast<hipEvent_t>(stop_event);
     return OFD_FW_OK;
+}
+
+int ofd_fw_set_disparity_rows(int on) {
+    const int prev = disp_row_enabled() ? 1 : 0;
+    if (on == 0 || on == 1) g_disp_rows = on;
+    return prev;
 }
 
 int ofd_fw_set_engine(int engine) {

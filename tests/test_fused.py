@@ -42,10 +42,20 @@ def test_unfused_reference_sequence_on_cpu_matches_fixture_flow():
     assert np.array_equal(flow[0].numpy(), g["img0/flow01"])
 
 
+@pytest.fixture(params=[1, 0], ids=["rows", "tile"])
+def disparity_engine(request):
+    """The disparity warps' row kernel (default) and the TILE engine."""
+    from opticalflowfromdepth_amd import _native
+    lib = _native.lib()
+    prev = lib.ofd_fw_set_disparity_rows(request.param)
+    yield request.param
+    lib.ofd_fw_set_disparity_rows(prev)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
 @pytest.mark.parametrize("shape,extra", [((3, 48, 64), 0), ((2, 37, 53), 1), ((1, 2, 9), 0), ((2, 96, 128), 2)])
-def test_warp_disparity_bit_exact(dtype, shape, extra):
+def test_warp_disparity_bit_exact(dtype, shape, extra, disparity_engine):
     from opticalflowfromdepth_amd import forward_warp_flow, warp_disparity
     B, H, W = shape
     rgb, d, s, ex = _inputs(B, H, W, dtype, 100 + H, extra)
@@ -90,7 +100,7 @@ def test_warp_disparity_headline_batch():
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
 @pytest.mark.parametrize("W", [64, 53])
-def test_warp_disparity_special_depths(dtype, W):
+def test_warp_disparity_special_depths(dtype, W, disparity_engine):
     """The row kernel (one workgroup per image row, 16-byte and scalar lanes)
     on depths the reference's z-test treats specially: 0 (infinite disparity,
     clamped onto column 0), NaN (dropped), >= 1000 (lands, never wins: a

@@ -65,6 +65,17 @@ def test_engine_switch():
     lib.ofd_fw_set_engine(cur)
 
 
+def test_disparity_rows_switch():
+    from opticalflowfromdepth_amd import _native
+    lib = _native.lib()
+    cur = lib.ofd_fw_set_disparity_rows(-1)
+    assert cur in (0, 1)
+    assert lib.ofd_fw_set_disparity_rows(0) == cur
+    assert lib.ofd_fw_set_disparity_rows(1) == 0
+    assert lib.ofd_fw_set_disparity_rows(-1) == 1
+    lib.ofd_fw_set_disparity_rows(cur)
+
+
 def test_argument_errors_without_gpu():
     """Validation happens before any HIP call, so it is testable on CPU."""
     from opticalflowfromdepth_amd import _native
