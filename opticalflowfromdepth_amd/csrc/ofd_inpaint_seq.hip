@@ -1597,16 +1597,17 @@ __global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, int C, int H, 
                 // code 0: (v1 - v2) * 2, 1: (v1 - v0), 2: (v3 - v2), 3: none ((v0 - v0) * 0 = +0)
                 const uint32_t xa = cx <= 1u ? w1 : (cx == 2u ? w3 : w0), xb = (cx & 1u) ? w0 : w2;
                 const uint32_t ya = cy <= 1u ? w4 : (cy == 2u ? w6 : w0), yb = (cy & 1u) ? w0 : w5;
-                const float fx = cx == 0u ? 2.0f : (cx == 3u ? 0.0f : 1.0f);
-                const float fy = cy == 0u ? 2.0f : (cy == 3u ? 0.0f : 1.0f);
-                const float ry = float(-a), rx = float(-b);
+                // gix * rx = (A - B) * (f * rx) exactly: integers below 2^24 (the
+                // sign of an exact zero may differ, which no result can see)
+                const float kx = (cx == 0u ? 2.0f : (cx == 3u ? 0.0f : 1.0f)) * float(-b);
+                const float ky = (cy == 0u ? 2.0f : (cy == 3u ? 0.0f : 1.0f)) * float(-a);
                 const bool live = gl + kL3 * k < kDisk;
 #pragma unroll
                 for (int c = 0; c < 3; ++c) {
-                    auto ch = [&](uint32_t q) -> float { return float((q >> (8 * c)) & 0xFFu); };
-                    const float vs = ch(w0);
-                    const float gix = (ch(xa) - ch(xb)) * fx, giy = (ch(ya) - ch(yb)) * fy;
-                    const float ta = wt * vs, tx = wt * (gix * rx), ty = wt * (giy * ry);
+                    auto byte = [&](uint32_t q) -> int { return int((q >> (8 * c)) & 0xFFu); };
+                    const float vs = float(byte(w0));
+                    const float dx = float(byte(xa) - byte(xb)), dy = float(byte(ya) - byte(yb));
+                    const float ta = wt * vs, tx = wt * (dx * kx), ty = wt * (dy * ky);
                     if (c == 0) {
                         t0[k][0] = ta;
                         t0[k][1] = tx;
