@@ -342,7 +342,12 @@ struct FmmLds {
     uint32_t nd, ovf;
 };
 
-__device__ __forceinline__ uint32_t bucket_of(float T) { return uint32_t(T * 2.0f); }
+// Bucket k holds T in [k w, (k + 1) w) with w = 1 / bscale.  A push lands at
+// least 1/sqrt(2) above the bucket's smallest pop (less float rounding of T:
+// half an ulp, under 2^-11 for T < 8192), so any w <= 0.7 keeps every push
+// out of its own bucket: w = 0.7 while H + W < 8000 bounds T, else 0.5.
+// (Double product: the bucket edges are exact to far below the margin.)
+__device__ __forceinline__ uint32_t bucket_of(float T, double bscale) { return uint32_t(double(T) * bscale); }
 
 // distance of padded pixel p pushed with seq s: FastMarching_solve over the
 // neighbours reached before it (stamp < s); cv2's fm order (up/left,
@@ -606,7 +611,8 @@ constexpr int kFB = OFD_FMM_B;
 // every push's stamp, distance and log entry; returns the number of log
 // entries (band + pushes).
 template <bool kInner>
-__device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L, uint32_t &nbuckets, uint64_t *prof) {
+__device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L, uint32_t &nbuckets, uint64_t *prof,
+                         double bscale) {
     (void)prof;
     const int tid = threadIdx.x, ew = m.ew;
     const int64_t off[4] = {-int64_t(ew), -1, int64_t(ew), 1};  // cv2's q = 0..3: up, left, down, right
@@ -623,7 +629,7 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
             lo = k >= 3 ? start[(k - 3) & 3] : nb;
             if (lo == seq) break;  // nothing pending in buckets >= k
         }
-        if (k > 4u * uint32_t(m.en) + 16u) {  // cannot happen: bucket k holds T >= k/2 and T < en
+        if (k > 4u * uint32_t(m.en) + 16u) {  // cannot happen: bucket k holds T >= k w >= k / 2 and T < en
             if (tid == 0) m.meta[5] = 1u;
             break;
         }
@@ -643,7 +649,7 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
             for (int u = 0; u < kFB; ++u) {
                 const uint32_t i = b + kFB * tid + u;
                 T[u] = i < hi ? m.logt[i] : 0.f;
-                if (i < hi && bucket_of(T[u]) == k) sel |= 1u << u;
+                if (i < hi && bucket_of(T[u], bscale) == k) sel |= 1u << u;
             }
             uint32_t tot;
             uint32_t pos = block_scan(__popc(sel), tot, L.scr);
@@ -907,7 +913,7 @@ __device__ __forceinline__ Img outer_view(const Img &m) {
 // They touch disjoint pixels (ring pixels are not 4-adjacent to holes) and
 // keep separate stamps, logs and sort buffers; the only value both read is
 // the band's zero distance (band_t).
-__global__ __launch_bounds__(kThreads) void sq_fmm_kernel(SqWs w) {
+__global__ __launch_bounds__(kThreads) void sq_fmm_kernel(SqWs w, double bscale) {
     __shared__ FmmLds L;
     const Img m = image(w, blockIdx.x);
     const uint32_t nb = m.meta[0];
@@ -915,7 +921,7 @@ __global__ __launch_bounds__(kThreads) void sq_fmm_kernel(SqWs w) {
     uint64_t prof[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     if (blockIdx.y == 0) {
         const Img o = outer_view(m);
-        const uint32_t no = fmm_pass<false>(o, m.sO, nb, L, nbk, prof);
+        const uint32_t no = fmm_pass<false>(o, m.sO, nb, L, nbk, prof, bscale);
         for (uint32_t i = threadIdx.x; i < no; i += kThreads) {
             const uint32_t p = o.logp[i];
             m.t[p] = -m.t[p];
@@ -923,7 +929,7 @@ __global__ __launch_bounds__(kThreads) void sq_fmm_kernel(SqWs w) {
         if (threadIdx.x == 0) atomicAdd(&m.meta[4], nbk);
         return;
     }
-    const uint32_t ni = fmm_pass<true>(m, m.sI, nb, L, nbk, prof);
+    const uint32_t ni = fmm_pass<true>(m, m.sI, nb, L, nbk, prof, bscale);
     if (threadIdx.x == 0) {
         m.meta[1] = ni - nb;
         m.meta[2] = 0u;
@@ -1748,6 +1754,11 @@ int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float 
         return e && e[0] == 'g';
     }();
     const bool rec3 = r == 3 && C <= 3 && en < (int64_t(1) << 26) && !force_g16;
+    static const double wide = [] {  // OFD_SEQ_BUCKET=0.5 selects the narrow buckets (A/B)
+        const char *e = getenv("OFD_SEQ_BUCKET");
+        return e ? atof(e) : 0.7;
+    }();
+    const double bscale = (H + W < 8000 && wide > 0.0 && wide <= 0.7) ? 1.0 / wide : 2.0;
     for (int64_t b0 = 0; b0 < B; b0 += G) {
         const int64_t nb = B - b0 < G ? B - b0 : G;
         hipLaunchKernelGGL(sq_prep_kernel, dim3(unsigned((W + 63) / 64), unsigned((H + 3) / 4), unsigned(nb)), dim3(256),
@@ -1755,7 +1766,7 @@ int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float 
         hipLaunchKernelGGL(sq_init_kernel, dim3(unsigned((w.eh + 3) / 4), unsigned(nb)), dim3(256), 0, st, w, r);
         hipLaunchKernelGGL(sq_band_scan_kernel, dim3(unsigned(nb)), dim3(kThreads), 0, st, w);
         hipLaunchKernelGGL(sq_band_write_kernel, dim3(unsigned((w.eh + 3) / 4), unsigned(nb)), dim3(256), 0, st, w);
-        hipLaunchKernelGGL(sq_fmm_kernel, dim3(unsigned(nb), 2u), dim3(kThreads), 0, st, w);
+        hipLaunchKernelGGL(sq_fmm_kernel, dim3(unsigned(nb), 2u), dim3(kThreads), 0, st, w, bscale);
         if (rec3) {
             hipLaunchKernelGGL(sq_record3_kernel, dim3(unsigned((w.ew + 63) / 64), unsigned((w.eh + 3) / 4), unsigned(nb)),
                                dim3(256), 0, st, w);
