@@ -49,7 +49,24 @@ def build_native(force: bool = False, verbose: bool = False) -> str:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
     os.replace(tmp, OUT)  # atomic: concurrent builders never expose a half-written .so
+    build_c_host()
     return OUT
+
+
+HOST_SRC = os.path.join(REPO, "tests", "c_host", "ofd_host.c")
+HOST_OUT = os.path.join(OUT_DIR, "ofd_host")
+
+
+def build_c_host() -> str:
+    """tests/c_host/ofd_host.c: the C ABI driven from plain C (gcc, libamdhip64), for tests/test_c_host.py."""
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    tmp = HOST_OUT + f".tmp{os.getpid()}"
+    subprocess.run(["gcc", "-std=c99", "-O2", "-Wall", "-D__HIP_PLATFORM_AMD__", "-I", os.path.join(REPO, "include"),
+                    "-I", os.path.join(rocm, "include"), "-o", tmp, HOST_SRC, "-L", OUT_DIR, "-lofd_fw",
+                    "-L", os.path.join(rocm, "lib"), "-lamdhip64", f"-Wl,-rpath,{OUT_DIR}",
+                    f"-Wl,-rpath,{os.path.join(rocm, 'lib')}", "-Wl,-rpath,$ORIGIN"], check=True)
+    os.replace(tmp, HOST_OUT)
+    return HOST_OUT
 
 
 if __name__ == "__main__":
