@@ -288,11 +288,14 @@ def augment_flow_batch(img0, img0_depth, img1, img1_depth, flow01, back_flow01, 
                                                torch.zeros(B), dev)
         a0_flow, _ = cf(bsf, sf, flow01, img0_depth)
         a1_flow, _ = cf(flow01, back_flow01, sf, img1_depth)
-        a0_all, valid, coll = fw(torch.cat((img0, img0_depth), 1), sf, img0_depth)
-        a0 = inpaint_(a0_all[:, 0:3], valid, coll)
+        a0_all, valid0, coll0 = fw(torch.cat((img0, img0_depth), 1), sf, img0_depth)
+        a1_all, valid1, coll1 = fw(torch.cat((img1, img1_depth), 1), sf, img1_depth)
+        # the two hole-fills (:164, :170) in one call over 2B images: the fill
+        # is per image, and one launch keeps twice the workgroups busy
+        a01 = inpaint_(torch.cat((a0_all[:, 0:3], a1_all[:, 0:3])), torch.cat((valid0, valid1)),
+                       torch.cat((coll0, coll1)))
+        a0, a1 = a01[:B], a01[B:]
         a0_depth = fix_warped_depth(a0_all[:, 3:4])
-        a1_all, valid, coll = fw(torch.cat((img1, img1_depth), 1), sf, img1_depth)
-        a1 = inpaint_(a1_all[:, 0:3], valid, coll)
         a1_depth = fix_warped_depth(a1_all[:, 3:4])
         back_a0_flow, _ = bf(a0_flow, a0_depth)
         back_a1_flow, _ = bf(a1_flow, img0_depth)
@@ -387,52 +390,60 @@ class PreprocessPlusAugment(nn.Module):
         img1_depth = img1_depth * img1_valid
         back_flow01 = back_flow01 * img1_valid
         img1_depth = fix_warped_depth(img1_depth)
-        img1 = self.inpaint_fn(img1, img1_valid, coll)                                         # :366
+        coll1 = coll
 
-        # :372-373 (and :385-387 below): the ego-motion flow plane is kept (it
-        # is a group output); the warp derives the same flow in-kernel and
-        # generates obj's depth / flow channels (bit-identical to
-        # fw(cat(img1, img1_depth, flow12 * -1.0, img1_valid), flow12, img1_depth))
+        # :385-387 -- independent of img1's fill, so its hole-fill shares one
+        # call with img1's (the fill is per image; one launch over 2B images
+        # keeps twice the workgroups busy).  The ego-motion flow plane is
+        # kept (a group output); the fused warp derives the same flow
+        # in-kernel and generates obj's depth / flow channels.
         P, ik = synth.projection(img0.shape[-2], img0.shape[-1], T1, img0.device)
+        flow03, _ = Convert.depth_to_random_flow(img0_depth, T1=T1)                    # :385
+        o, img3_valid, coll3 = warp_ego(img0.to(torch.float32).contiguous(), img0_depth.contiguous(), P, ik)
+        img3, img3_depth, back_flow03 = o[:, 0:3], o[:, 3:4], o[:, 4:6]
+        img3 = img3 * img3_valid
+        img3_depth = img3_depth * img3_valid
+        back_flow03 = back_flow03 * img3_valid
+        B = img1.shape[0]
+        f13 = self.inpaint_fn(torch.cat((img1, img3)), torch.cat((img1_valid, img3_valid)),
+                              torch.cat((coll1, coll3)))                                          # :366, :391
+        img1, img3 = f13[:B], f13[B:]
+        img3_depth = fix_warped_depth(img3_depth)
+
+        # :372-373: bit-identical to
+        # fw(cat(img1, img1_depth, flow12 * -1.0, img1_valid), flow12, img1_depth)
         flow12, _ = Convert.depth_to_random_flow(img1_depth, T1=T1)                    # :372
-        o, valid, coll = warp_ego(torch.cat((img1, img1_valid), 1), img1_depth.contiguous(), P, ik)
+        o, valid, coll2 = warp_ego(torch.cat((img1, img1_valid), 1), img1_depth.contiguous(), P, ik)
         img2, img2_depth, back_flow12, fw_img1_valid = o[:, 0:3], o[:, 3:4], o[:, 4:6], o[:, 6:7]
         img2_valid = valid * fw_img1_valid
         img2 = img2 * img2_valid
         img2_depth = img2_depth * img2_valid
         back_flow12 = back_flow12 * img2_valid
-        img2 = self.inpaint_fn(img2, img2_valid, coll)
         img2_depth = fix_warped_depth(img2_depth)
 
-        flow03, _ = Convert.depth_to_random_flow(img0_depth, T1=T1)                    # :385
-        o, img3_valid, coll = warp_ego(img0.to(torch.float32).contiguous(), img0_depth.contiguous(), P, ik)
-        img3, img3_depth, back_flow03 = o[:, 0:3], o[:, 3:4], o[:, 4:6]
-        img3 = img3 * img3_valid
-        img3_depth = img3_depth * img3_valid
-        back_flow03 = back_flow03 * img3_valid
-        img3 = self.inpaint_fn(img3, img3_valid, coll)
-        img3_depth = fix_warped_depth(img3_depth)
-
         flow02, flow02_valid = cf(flow01, back_flow01, flow12, img1_depth)             # :400
-        o, valid, coll = fw(torch.cat((img0, img0_depth, flow02 * -1.0, flow02_valid), 1), flow02, img0_depth)
+        o, valid, coll2p = fw(torch.cat((img0, img0_depth, flow02 * -1.0, flow02_valid), 1), flow02, img0_depth)
         img2p, img2p_depth, back_flow02p, fw_flow02_valid = o[:, 0:3], o[:, 3:4], o[:, 4:6], o[:, 6:7]
         img2p_valid = valid * fw_flow02_valid
         img2p = img2p * img2p_valid
         img2p_depth = img2p_depth * img2p_valid
         back_flow02p = back_flow02p * img2p_valid
-        img2p = self.inpaint_fn(img2p, img2p_valid, coll)
         img2p_depth = fix_warped_depth(img2p_depth)
 
         flow13, flow13_valid = cf(back_flow01, flow01, flow03, img1_depth)             # :414
         flow13_valid = flow13_valid * img1_valid
-        o, valid, coll = fw(torch.cat((img1, img1_depth, flow13 * -1.0, flow13_valid), 1), flow13, img1_depth)
+        o, valid, coll3p = fw(torch.cat((img1, img1_depth, flow13 * -1.0, flow13_valid), 1), flow13, img1_depth)
         img3p, img3p_depth, back_flow13p, fw_flow13_valid = o[:, 0:3], o[:, 3:4], o[:, 4:6], o[:, 6:7]
         img3p_valid = valid * fw_flow13_valid
         img3p = img3p * img3p_valid
         img3p_depth = img3p_depth * img3p_valid
         back_flow13p = back_flow13p * img3p_valid
-        img3p = self.inpaint_fn(img3p, img3p_valid, coll)
         img3p_depth = fix_warped_depth(img3p_depth)
+
+        # the three remaining hole-fills (:379, :407, :421) in one call over 3B images
+        f = self.inpaint_fn(torch.cat((img2, img2p, img3p)), torch.cat((img2_valid, img2p_valid, img3p_valid)),
+                            torch.cat((coll2, coll2p, coll3p)))
+        img2, img2p, img3p = f[:B], f[B:2 * B], f[2 * B:]
 
         groups = [(img0, img0_depth, img1, img1_depth, flow01, back_flow01),           # :427-432
                   (img1, img1_depth, img2, img2_depth, flow12, back_flow12),
