@@ -295,3 +295,21 @@ def test_layered_vs_sequential_divergence_on_warped_images():
     stats = dict(mean=float(d.mean()), p99=float(np.percentile(d, 99)), frac_over_8=float((d > 8).mean()),
                  frac_over_32=float((d > 32).mean()))
     assert stats["mean"] < 8.0 and stats["p99"] < 64 and stats["frac_over_32"] < 0.05, stats
+
+
+@pytest.mark.gpu
+def test_inpaint_sequential_wide_image_half_unit_buckets():
+    """H + W >= 8000 takes the half-unit distance buckets (the 0.7-wide ones
+    need T < 8192); a long strip with holes of every kind, cv2 order, bit-exact."""
+    from opticalflowfromdepth_amd import ops
+    rng = np.random.default_rng(21)
+    h, w = 10, 8200
+    img = rng.integers(0, 256, (1, 3, h, w)).astype(np.float32)
+    v = (rng.random((1, 1, h, w)) < 0.7).astype(np.float32)
+    v[..., :, 100:400] = 0  # a wide hole
+    v[..., :, -50:] = 0     # a border band
+    c = ((rng.random((1, 1, h, w)) < 0.05) & (v > 0)).astype(np.float32)
+    dev = torch.device("cuda:0")
+    got = ops.inpaint(torch.from_numpy(img * v).to(dev), torch.from_numpy(v).to(dev), torch.from_numpy(c).to(dev),
+                      order="sequential").cpu().numpy()
+    assert np.array_equal(got, oracle.inpaint(img * v, v, c, 3, layered=False))
