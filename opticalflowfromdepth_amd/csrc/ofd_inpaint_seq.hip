@@ -635,6 +635,9 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
         }
         start[k & 3] = seq;
         SQ_T(f0);
+#ifdef OFD_BUCKET_TRACE
+        const uint64_t tb0 = __builtin_amdgcn_s_memtime();
+#endif
         // gather bucket k in push order
         if (tid == 0) {
             L.tmin = INF;
@@ -827,6 +830,16 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
             sync_all();
             SQ_T(f6a);
             SQ_ACC(pb + 5, f5a, f6a);
+#ifdef OFD_BUCKET_TRACE
+            if (kInner && threadIdx.x == 0 && 8 * m.en + 4 * nbuckets + 4 < 40 * m.en) {
+                uint32_t *tr = m.rec + 8 * m.en + 4 * (nbuckets - 1);
+                tr[0] = uint32_t((__builtin_amdgcn_s_memtime() - tb0) >> 4);
+                tr[1] = n;
+                tr[2] = npush;
+                tr[3] = k;
+                m.rec[8 * m.en + 4 * m.en] = nbuckets;
+            }
+#endif
             continue;
         }
         // More pushes: sweep 0 evaluates every push; each later sweep only the
@@ -892,6 +905,16 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
         sync_all();
         SQ_T(f6);
         SQ_ACC(pb + 5, f5, f6);
+#ifdef OFD_BUCKET_TRACE
+        if (kInner && threadIdx.x == 0 && 8 * m.en + 4 * nbuckets + 4 < 40 * m.en) {
+            uint32_t *tr = m.rec + 8 * m.en + 4 * (nbuckets - 1);
+            tr[0] = uint32_t((__builtin_amdgcn_s_memtime() - tb0) >> 4);
+            tr[1] = n;
+            tr[2] = npush;
+            tr[3] = k;
+            m.rec[8 * m.en + 4 * m.en] = nbuckets;
+        }
+#endif
     }
     return seq;
 }
@@ -1767,6 +1790,9 @@ int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float 
         hipLaunchKernelGGL(sq_band_scan_kernel, dim3(unsigned(nb)), dim3(kThreads), 0, st, w);
         hipLaunchKernelGGL(sq_band_write_kernel, dim3(unsigned((w.eh + 3) / 4), unsigned(nb)), dim3(256), 0, st, w);
         hipLaunchKernelGGL(sq_fmm_kernel, dim3(unsigned(nb), 2u), dim3(kThreads), 0, st, w, bscale);
+#ifdef OFD_BUCKET_TRACE
+        continue;  // probe: keep the record area (the inner march's bucket trace) for the host
+#endif
         if (rec3) {
             hipLaunchKernelGGL(sq_record3_kernel, dim3(unsigned((w.ew + 63) / 64), unsigned((w.eh + 3) / 4), unsigned(nb)),
                                dim3(256), 0, st, w);
