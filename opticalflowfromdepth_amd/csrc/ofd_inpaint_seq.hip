@@ -645,7 +645,14 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
         }
         __syncthreads();
         uint32_t n = 0, tmn = INF, tmx = 0u;
-        for (uint32_t b = lo; b < hi; b += kFB * kThreads) {  // 4 consecutive entries per thread: one load round
+        // bucket 0 is the band: every log entry [0, nb), all at T = 0, already
+        // in (T, push order) -- its pops are the log itself (no gather, no sort)
+        const bool band = k == 0;
+        if (band) {
+            n = nb;
+            tmn = tmx = 0u;
+        }
+        for (uint32_t b = band ? hi : lo; b < hi; b += kFB * kThreads) {  // kFB consecutive entries per thread
             float T[kFB];
             unsigned sel = 0;
 #pragma unroll
@@ -684,7 +691,9 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
         __syncthreads();
         const bool uniform = L.tmin == L.tmax;  // already in (T, seq) order
         const uint64_t *keys = L.keys;
-        if (n > kCap) {
+        if (band) {
+            keys = nullptr;  // pop rank r is log entry r
+        } else if (n > kCap) {
             for (int i = tid; i < kCap; i += kThreads) m.k0[i] = L.keys[i];
             sync_all();
             keys = uniform ? m.k0 : (digit_sort(m.k0, m.k1, n, L) ? m.k1 : global_sort(m.k0, m.k1, n, L));
@@ -700,7 +709,7 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
 #pragma unroll
             for (int u = 0; u < kFB; ++u) {
                 const uint32_t r = r0 + uint32_t(u) * kThreads;
-                a[u] = r < n ? int64_t(m.logp[uint32_t(keys[r])]) : 0;
+                a[u] = r < n ? int64_t(m.logp[keys ? uint32_t(keys[r]) : r]) : 0;
             }
 #pragma unroll
             for (int u = 0; u < kFB; ++u)
@@ -724,7 +733,7 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
 #pragma unroll
             for (int u = 0; u < kFB; ++u) {
                 const uint32_t r = b + uint32_t(u) * kThreads + tid;
-                a[u] = r < n ? int64_t(m.logp[uint32_t(keys[r])]) : 0;
+                a[u] = r < n ? int64_t(m.logp[keys ? uint32_t(keys[r]) : r]) : 0;
             }
 #pragma unroll
             for (int u = 0; u < kFB; ++u)
