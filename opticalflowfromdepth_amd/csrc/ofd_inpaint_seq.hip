@@ -1591,8 +1591,18 @@ __global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, int C, int H, 
                 }
             }
             SQ_T(c0a);
+            float *bf = L.buf[g];
+            uint32_t *gv = reinterpret_cast<uint32_t *>(bf);
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                if (gl + kL3 * k < kVal3) gv[VC(k)] = v[k];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             // release the later holes that read this one (their counters
-            // reach zero only after this level's barrier is passed)
+            // reach zero only after this level's barrier is passed).  Issued
+            // after the loads have landed, so no wait for the loads also
+            // waits for these: their round trip overlaps the arithmetic.
             const uint64_t dep = uint64_t(mq.x) | (uint64_t(mq.y) << 32);
             uint32_t old[8];
 #pragma unroll
@@ -1604,14 +1614,6 @@ __global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, int C, int H, 
                 }
             }
             SQ_T(c1);
-            float *bf = L.buf[g];
-            uint32_t *gv = reinterpret_cast<uint32_t *>(bf);
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-                if (gl + kL3 * k < kVal3) gv[VC(k)] = v[k];
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             // this lane's terms (disk positions gl + 8k): channels 1 and 2 go
             // to LDS at once (past the grid), channel 0 waits in registers
             // until every lane of the hole is done with the grid
