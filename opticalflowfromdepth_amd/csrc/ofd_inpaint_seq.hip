@@ -1402,6 +1402,10 @@ constexpr int kSlots3 = 1024 / kL3;      // holes in flight per workgroup
 constexpr int kVal3 = 61;                // window (disk dilated by 3x3) incl. the centre
 constexpr int kTerm3 = 9 * kDisk;        // 3 channels x (Ia, Jx, Jy) x disk positions
 constexpr int kFrCap = 1280;             // LDS frontier entries per buffer
+// a hole's LDS slot stride: >= kTerm3 and = 8 (mod 64 banks), so the 8 holes
+// x 8 lanes of a wave hit 64 distinct banks on lane-contiguous accesses
+constexpr int kBufStride = (kTerm3 + 55) / 64 * 64 + 8;
+static_assert(kBufStride >= kTerm3 && kBufStride % 64 == 8, "slot stride");
 
 // e-th position (raster order) of the window including its centre
 __device__ __forceinline__ void val_pos(int e, int &a, int &b) {
@@ -1522,7 +1526,7 @@ __global__ __launch_bounds__(256) void sq_record3_kernel(SqWs w) {
 struct C3Lds {
     uint32_t nnext;
     uint64_t fr[2][kFrCap];
-    float buf[kSlots3][kTerm3];  // per hole: the 9x9 colour grid (81 words), then the terms
+    float buf[kSlots3][kBufStride];  // per hole: the 9x9 colour grid (81 words), then the terms
     float res[kSlots3][9];       // per hole: chain results (Ia, Jx, Jy per channel)
 };
 
