@@ -840,13 +840,13 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
             SQ_T(f6a);
             SQ_ACC(pb + 5, f5a, f6a);
 #ifdef OFD_BUCKET_TRACE
-            if (kInner && threadIdx.x == 0 && 8 * m.en + 4 * nbuckets + 4 < 40 * m.en) {
-                uint32_t *tr = m.rec + 8 * m.en + 4 * (nbuckets - 1);
+            if (threadIdx.x == 0 && 4 * nbuckets + 4 < 4 * m.en) {  // inner at 8 en, outer at 20 en
+                uint32_t *tr = m.rec + (kInner ? 8 : 20) * m.en + 4 * (nbuckets - 1);
                 tr[0] = uint32_t((__builtin_amdgcn_s_memtime() - tb0) >> 4);
                 tr[1] = n;
                 tr[2] = npush;
                 tr[3] = k;
-                m.rec[8 * m.en + 4 * m.en] = nbuckets;
+                m.rec[(kInner ? 8 : 20) * m.en + 4 * m.en] = nbuckets;
             }
 #endif
             continue;
@@ -915,13 +915,13 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
         SQ_T(f6);
         SQ_ACC(pb + 5, f5, f6);
 #ifdef OFD_BUCKET_TRACE
-        if (kInner && threadIdx.x == 0 && 8 * m.en + 4 * nbuckets + 4 < 40 * m.en) {
-            uint32_t *tr = m.rec + 8 * m.en + 4 * (nbuckets - 1);
+        if (threadIdx.x == 0 && 4 * nbuckets + 4 < 4 * m.en) {  // inner at 8 en, outer at 20 en
+            uint32_t *tr = m.rec + (kInner ? 8 : 20) * m.en + 4 * (nbuckets - 1);
             tr[0] = uint32_t((__builtin_amdgcn_s_memtime() - tb0) >> 4);
             tr[1] = n;
             tr[2] = npush;
             tr[3] = k;
-            m.rec[8 * m.en + 4 * m.en] = nbuckets;
+            m.rec[(kInner ? 8 : 20) * m.en + 4 * m.en] = nbuckets;
         }
 #endif
     }
