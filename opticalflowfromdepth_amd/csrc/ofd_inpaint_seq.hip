@@ -467,7 +467,8 @@ __device__ __forceinline__ uint32_t hfind(const FmmLds &L, uint32_t v) {
 // 1024-key chunk at a time (rank within a value = earlier lanes of the wave
 // with that value + earlier waves + earlier chunks).  Returns false, having
 // written nothing, when there are more distinct values.
-__device__ bool digit_sort(const uint64_t *g, uint64_t *out, uint32_t n, FmmLds &L) {
+__device__ bool digit_sort(const uint64_t *g, uint64_t *out, uint32_t n, FmmLds &L, const uint32_t *logp = nullptr,
+                           uint32_t *outp = nullptr) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     for (int i = tid; i < kHash; i += kThreads) {
         L.hk[i] = INF;
@@ -556,6 +557,7 @@ __device__ bool digit_sort(const uint64_t *g, uint64_t *out, uint32_t n, FmmLds 
             uint32_t pre = 0;
             for (int w2 = 0; w2 < wave; ++w2) pre += L.wc[w2][d];
             out[L.base[d] + pre + r] = key;
+            if (outp) outp[L.base[d] + pre + r] = logp[uint32_t(key)];  // the pop's pixel, by rank
         }
         __syncthreads();
         if (uint32_t(tid) < nd) {
@@ -691,12 +693,23 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
         __syncthreads();
         const bool uniform = L.tmin == L.tmax;  // already in (T, seq) order
         const uint64_t *keys = L.keys;
+        const uint32_t *kpx = nullptr;  // pixel of each pop by rank, when the sort provides it
         if (band) {
             keys = nullptr;  // pop rank r is log entry r
         } else if (n > kCap) {
             for (int i = tid; i < kCap; i += kThreads) m.k0[i] = L.keys[i];
             sync_all();
-            keys = uniform ? m.k0 : (digit_sort(m.k0, m.k1, n, L) ? m.k1 : global_sort(m.k0, m.k1, n, L));
+            // the counting sort also lays the pops' pixels out by rank (the
+            // claims and pushes of these long buckets then skip one dependent
+            // load per pop); the area is free until RECORD
+            uint32_t *rank_px = m.rec + (kInner ? 7 : 6) * m.en;
+            if (uniform)
+                keys = m.k0;
+            else if (digit_sort(m.k0, m.k1, n, L, m.logp, rank_px)) {
+                keys = m.k1;
+                kpx = rank_px;
+            } else
+                keys = global_sort(m.k0, m.k1, n, L);
         } else if (!uniform && n > 1) {
             keys = lds_sort(L, n);
         }
@@ -709,7 +722,7 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
 #pragma unroll
             for (int u = 0; u < kFB; ++u) {
                 const uint32_t r = r0 + uint32_t(u) * kThreads;
-                a[u] = r < n ? int64_t(m.logp[keys ? uint32_t(keys[r]) : r]) : 0;
+                a[u] = r < n ? int64_t(kpx ? kpx[r] : m.logp[keys ? uint32_t(keys[r]) : r]) : 0;
             }
 #pragma unroll
             for (int u = 0; u < kFB; ++u)
@@ -733,7 +746,7 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
 #pragma unroll
             for (int u = 0; u < kFB; ++u) {
                 const uint32_t r = b + uint32_t(u) * kThreads + tid;
-                a[u] = r < n ? int64_t(m.logp[keys ? uint32_t(keys[r]) : r]) : 0;
+                a[u] = r < n ? int64_t(kpx ? kpx[r] : m.logp[keys ? uint32_t(keys[r]) : r]) : 0;
             }
 #pragma unroll
             for (int u = 0; u < kFB; ++u)
