@@ -683,6 +683,9 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
         }
         SQ_T(f1);
         SQ_ACC(0, f0, f1);
+#ifdef OFD_BUCKET_TRACE
+        const uint64_t tb1 = __builtin_amdgcn_s_memtime();
+#endif
         if (n == 0) continue;
         ++nbuckets;
 #ifdef OFD_SQ_PROF
@@ -715,6 +718,9 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
         }
         SQ_T(f2);
         SQ_ACC(pb + 1, f1, f2);
+#ifdef OFD_BUCKET_TRACE
+        const uint64_t tb2 = __builtin_amdgcn_s_memtime();
+#endif
         // pops in order: claim the INSIDE neighbours (first claimant = pusher)
         for (uint32_t r0 = tid; r0 < n; r0 += kFB * kThreads) {  // 4 pops per thread: one round per load step
             int64_t a[kFB];
@@ -738,6 +744,9 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
         sync_all();
         SQ_T(f3);
         SQ_ACC(pb + 2, f2, f3);
+#ifdef OFD_BUCKET_TRACE
+        const uint64_t tb3 = __builtin_amdgcn_s_memtime();
+#endif
         // pushes numbered in (rank, direction) order
         uint32_t npush = 0;
         for (uint32_t b = 0; b < n; b += kFB * kThreads) {  // kFB slices of kThreads ranks, loads first
@@ -780,6 +789,9 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
         sync_all();
         SQ_T(f4);
         SQ_ACC(pb + 3, f3, f4);
+#ifdef OFD_BUCKET_TRACE
+        const uint64_t tb4 = __builtin_amdgcn_s_memtime();
+#endif
         // distances: sweep to the fixed point (acyclic in push order: at most
         // npush + 1 sweeps; the cap only guards against a broken invariant).
         // Up to kLdsPush pushes: the bucket's distances live in LDS and each
@@ -853,9 +865,13 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
             SQ_T(f6a);
             SQ_ACC(pb + 5, f5a, f6a);
 #ifdef OFD_BUCKET_TRACE
-            if (threadIdx.x == 0 && 4 * nbuckets + 4 < 4 * m.en) {  // inner at 8 en, outer at 20 en
-                uint32_t *tr = m.rec + (kInner ? 8 : 20) * m.en + 4 * (nbuckets - 1);
+            if (threadIdx.x == 0 && 8 * nbuckets + 8 < 4 * m.en) {  // inner at 8 en, outer at 20 en
+                uint32_t *tr = m.rec + (kInner ? 8 : 20) * m.en + 8 * (nbuckets - 1);
                 tr[0] = uint32_t((__builtin_amdgcn_s_memtime() - tb0) >> 4);
+                tr[4] = uint32_t((tb1 - tb0) >> 4);
+                tr[5] = uint32_t((tb2 - tb1) >> 4);
+                tr[6] = uint32_t((tb3 - tb2) >> 4);
+                tr[7] = uint32_t((tb4 - tb3) >> 4);
                 tr[1] = n;
                 tr[2] = npush;
                 tr[3] = k;
@@ -928,9 +944,13 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
         SQ_T(f6);
         SQ_ACC(pb + 5, f5, f6);
 #ifdef OFD_BUCKET_TRACE
-        if (threadIdx.x == 0 && 4 * nbuckets + 4 < 4 * m.en) {  // inner at 8 en, outer at 20 en
-            uint32_t *tr = m.rec + (kInner ? 8 : 20) * m.en + 4 * (nbuckets - 1);
+        if (threadIdx.x == 0 && 8 * nbuckets + 8 < 4 * m.en) {  // inner at 8 en, outer at 20 en
+            uint32_t *tr = m.rec + (kInner ? 8 : 20) * m.en + 8 * (nbuckets - 1);
             tr[0] = uint32_t((__builtin_amdgcn_s_memtime() - tb0) >> 4);
+            tr[4] = uint32_t((tb1 - tb0) >> 4);
+            tr[5] = uint32_t((tb2 - tb1) >> 4);
+            tr[6] = uint32_t((tb3 - tb2) >> 4);
+            tr[7] = uint32_t((tb4 - tb3) >> 4);
             tr[1] = n;
             tr[2] = npush;
             tr[3] = k;

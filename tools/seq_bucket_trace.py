@@ -38,13 +38,13 @@ for march, off in (("inner", 8), ("outer", 20)):
     base = rec0 + bl * en * 160
     q = (off * en + 4 * en) * 4
     nb = int(ws[base + q: base + q + 4].view(torch.int32).item())
-    tr = ws[base + off * en * 4: base + off * en * 4 + nb * 16].view(torch.int32).cpu().numpy().reshape(nb, 4)
+    tr = ws[base + off * en * 4: base + off * en * 4 + nb * 32].view(torch.int32).cpu().numpy().reshape(nb, 8)
     tot = int(tr[:, 0].astype(np.int64).sum())
     if best is None or tot > best[0]:
         best = (tot, bl, nb)
   _, bl, nb = best
   base = rec0 + bl * en * 160 + off * en * 4
-  tr = ws[base: base + nb * 16].view(torch.int32).cpu().numpy().reshape(nb, 4).astype(np.int64)
+  tr = ws[base: base + nb * 32].view(torch.int32).cpu().numpy().reshape(nb, 8).astype(np.int64)
   dur = tr[:, 0] * 16 / 2.4e3  # us at ~2.4 GHz
   n, npush = tr[:, 1], tr[:, 2]
   print(f"{march} march, slowest image {bl}: {nb} buckets, {dur.sum() / 1e3:.2f} ms (clock 2.4 GHz assumed)")
@@ -55,3 +55,10 @@ for march, off in (("inner", 8), ("outer", 20)):
               f"median {np.median(dur[sel]):7.1f} us, pushes {npush[sel].sum()}")
   print("  first 8 buckets (us, keys, pushes):",
         [(round(float(d), 1), int(a), int(b)) for d, a, b in zip(dur[:8], n[:8], npush[:8])])
+  ph = tr[:, 4:8] * 16 / 2.4e3
+  big = n > 4096
+  for name, sel in (("large", big), ("small", ~big)):
+      if sel.any():
+          g_, so, cl, pu = (ph[sel, c].sum() / 1e3 for c in range(4))
+          print(f"  {name} buckets: gather {g_:.2f}, sort {so:.2f}, claim {cl:.2f}, push {pu:.2f}, "
+                f"distances+log {dur[sel].sum() / 1e3 - g_ - so - cl - pu:.2f} ms")
