@@ -101,6 +101,19 @@ def cpu_model() -> str:
     return platform.processor() or platform.machine()
 
 
+def lease_cores(threads: int) -> dict:
+    """How many host cores the baseline may use, and why: the one-GPU lease's
+    CPU share is 16 cores (OMP_NUM_THREADS on the box); host_cpus counts the
+    whole machine, which the lease does not own."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = None
+    return {"affinity_cpus": aff, "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+            "cores_note": f"{threads} threads = the lease's CPU share (OMP_NUM_THREADS); "
+                          f"host_cpus is the whole machine, shared with other leases"}
+
+
 def timed_events(fn, steps, stream):
     """Mean ms per call of fn over `steps` calls, HIP events on `stream`."""
     fn()
@@ -180,7 +193,7 @@ def cpu_baseline(obj, flow, depth, budget_s, threads):
     warp_t = reps_t * n_img * H * W / el_t / 1e6
     flow_t = reps_f * n_img * H * W / el_f / 1e6
     return {"value": round(loop, 2), "unit": "Mpix/s", "cores": threads, "kind": "port",
-            "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
+            "cpu_model": cpu_model(), "host_cpus": os.cpu_count(), **lease_cores(threads),
             "sample": f"{n_img} images (of the {B}-image batch, both flow kinds) x {reps} reps, C={C}, "
                       f"{H}x{W}, oracle/fw_oracle.c serial-per-plane loop, {el:.1f} s wall",
             "torch_cpu": {"warp_scatter_amin_mpix_s": round(warp_t, 2),
@@ -306,7 +319,7 @@ def fused_ego_phase(B, H, W, steps, dev, stream):
     flow, the concatenation, then forward_warp_flow) and to the one-kernel
     flow plane (ops.ego_flow).  Algorithmic bytes of the fused call: RGB 12 +
     depth 8 in, 6 channels 24 + valid 4 + coll 4 out = 52 B/px."""
-    from opticalflowfromdepth_amd import ego_flow, forward_warp_flow, synth, warp_ego
+    from opticalflowfromdepth_amd import ego_flow, forward_warp_flow, synth, warp_ego, warp_flow_cat
     seeds = [12345 + i for i in range(B)]
     depth = synth.normalize_depth(synth.synthetic_depth(seeds, H, W, dev, dtype=torch.float64))
     rgb = synth.synthetic_rgb(seeds, H, W, dev)
@@ -322,12 +335,25 @@ def fused_ego_phase(B, H, W, steps, dev, stream):
     ms_unfused = timed_events(unfused, steps, stream)
     ms_flow = timed_events(lambda: ego_flow(depth, P, ik), steps, stream)
     ms_flow_torch = timed_events(lambda: synth.ego_motion_flow(depth, T), steps, stream)
+    # the honest comparator, and what the pipeline runs (the flow plane is a
+    # group output there): the HIP plane, then FW on it with obj's depth / flow
+    # channels generated (warp_flow_cat)
+    plane = ego_flow(depth, P, ik)
+    ms_cat = timed_events(lambda: warp_flow_cat(rgb, plane, depth), steps, stream)
     px = B * H * W
     gbs = px * 52 / (ms / 1e3) / 1e9
+    gbs_cat = px * 60 / (ms_cat / 1e3) / 1e9
     return {"metric": "Mpix/s fused depth->ego-motion flow->splat (preprocess.py:385-387), C=6 out",
             "value": round(px / (ms / 1e3) / 1e6, 1), "unit": "Mpix/s", "ms_per_step": round(ms, 4),
             "unfused_ms_per_step": round(ms_unfused, 4), "images": B, "steps": steps,
             "ego_flow_plane_ms": round(ms_flow, 4), "ego_flow_torch_ms": round(ms_flow_torch, 4),
+            "plane_then_warp_flow_cat": {
+                "warp_ms_per_step": round(ms_cat, 4), "plane_plus_warp_ms": round(ms_flow + ms_cat, 4),
+                "roofline": {"bound": "hbm", "achieved": round(gbs_cat, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": round(gbs_cat / HBM_PEAK_GBS, 4),
+                             "algorithmic_bytes_per_px": 60,
+                             "bytes": "RGB 12 + flow 8 + depth 8 in, 6 channels 24 + valid 4 + coll 4 out"},
+                "parity": "bit-exact vs FW on the materialised concatenation (tests/test_flow_cat.py)"},
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(gbs / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_px": 52},
             "parity": "bit-exact vs FW on ego_flow's plane; flow within 8 ulp of the reference's (tests/test_ego.py)"}
@@ -409,6 +435,29 @@ def config2_phase(steps, dev, stream, threads, cpu_budget):
     return rec
 
 
+# ---------------------------------------------------------------- multi-rank record
+def rank_report(ms_per_step: float, world: int, coll_dev) -> dict:
+    """What the process group saw: its size (dist.get_world_size(), not the
+    launcher's WORLD_SIZE), its backend, and every rank's own ms per step
+    (all_gather; the line's ms_per_step is the max-rank wall clock)."""
+    if world <= 1 or not dist.is_initialized():
+        return {"world_size": 1, "backend": None, "ms_per_step": [round(ms_per_step, 4)]}
+    n = dist.get_world_size()
+    mine = torch.tensor([ms_per_step], dtype=torch.float64, device=coll_dev)
+    got = [torch.zeros_like(mine) for _ in range(n)]
+    dist.all_gather(got, mine)
+    return {"world_size": n, "backend": dist.get_backend(), "ms_per_step": [round(float(x[0]), 4) for x in got]}
+
+
+def finish(world: int) -> None:
+    """Final barrier, then teardown: rank 0 runs its extra phases after the
+    timed steps, and no rank may tear the process group down while another
+    still uses it."""
+    if world > 1 and dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 # ---------------------------------------------------------------- main
 def dry_run(args, world, rank):
     """The launcher / collective / timing skeleton without a GPU (tests): gloo
@@ -430,15 +479,17 @@ def dry_run(args, world, rank):
         x += s_all[a:b]
     if world > 1:
         dist.barrier()
-    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    own = time.perf_counter() - t0
+    t = torch.tensor([own], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    ranks = rank_report(own * 1e3 / max(args.steps, 1), world, "cpu")
     if rank == 0:
-        print(json.dumps({"metric": METRIC, "value": None, "unit": "Mpix/s", "n_gpus": world,
+        time.sleep(0.2)  # stands in for rank 0's extra phases: the others wait at the final barrier
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "Mpix/s", "n_gpus": ranks["world_size"],
                           "steps": args.steps, "warmup": args.warmup, "dry_run": True,
-                          "shard_images": [a, b], "wall_s": float(t[0])}), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+                          "shard_images": [a, b], "wall_s": float(t[0]), "ranks": ranks}), flush=True)
+    finish(world)
 
 
 def main(argv=None):
@@ -526,6 +577,7 @@ def main(argv=None):
     rv_ms = [s.elapsed_time(e) for s, e in zip(rstarts, rends)] if evmode >= 1 else [dev_ms]
     resolve_ms = sum(rv_ms) / len(rv_ms)
 
+    ranks = rank_report(wall / args.steps * 1e3, world, coll_dev)
     t = torch.tensor([wall, dev_ms], dtype=torch.float64, device=coll_dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -593,7 +645,7 @@ def main(argv=None):
             "metric": METRIC,
             "value": round(value, 1),
             "unit": "Mpix/s",
-            "n_gpus": world,
+            "n_gpus": ranks["world_size"],
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(wall / args.steps * 1e3, 4),
@@ -625,10 +677,10 @@ def main(argv=None):
             "fused_disparity": fused,
             "fused_ego": fused_ego,
             "bf16_warp": bf16,
+            "ranks": ranks,
         }
         print(json.dumps(rec), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    finish(world)
 
 
 if __name__ == "__main__":

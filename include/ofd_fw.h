@@ -94,6 +94,16 @@ int ofd_fw_set_engine(int engine);
  * queries.  Returns the previous setting.  Process-wide, not thread-safe. */
 int ofd_fw_set_disparity_rows(int on);
 
+/* Row path of the TILE engine: images whose every source lands in its own row
+ * (BIN checks it per image and per call; e.g. any disparity flow,
+ * preprocess.py:249-254) are splatted row by row instead of through the tile
+ * lists; results are identical.  Used by the float32 / float64-flow / bf16
+ * flow entries and the forward_warping op when W <= 4096, W % 4 == 0 and every
+ * plane is 16-byte aligned (8-byte for bf16 planes).  on = 1 / 0 enables /
+ * disables it for subsequent calls (also OFD_FW_ROWPATH=0); any other value
+ * only queries.  Returns the previous setting.  Process-wide, not thread-safe. */
+int ofd_fw_set_row_path(int on);
+
 /* Benchmark hook: when non-NULL, the given hipEvent_t's are recorded on the
  * launch stream right before the first and right after the last launch of
  * each subsequent f32 call's dominant kernel: SPLAT (TILE engine), RESOLVE
@@ -208,6 +218,24 @@ int ofd_fw_warp_ego_f32(const float *obj, int64_t Cobj, const float *depth, cons
 int ofd_fw_warp_ego_f64depth(const float *obj, int64_t Cobj, const double *depth, const float *P,
                              const float *inv_K, float *output, float *valid, float *collision, int64_t B, int64_t H,
                              int64_t W, void *workspace, size_t workspace_bytes, void *stream);
+
+/* FW on a flow plane the caller holds, obj's depth and flow channels
+ * generated instead of concatenated: preprocess.py:371-373 / :385-387 (the
+ * ego-motion warps, whose flow planes are group outputs) and :400-402 /
+ * :414-417 (the composed-flow warps) all compute
+ *     obj_all = torch.cat((obj[:3], depth, flow * -1.0, obj[3:]))
+ *     FW(obj_all, flow, depth)
+ * This entry never stores obj_all: the winner's depth and flow * -1.0 are
+ * taken from the depth key and the flow plane.  obj [B,Cobj,H,W] f32 (the
+ * image and any appended channels, e.g. a validity mask); flow [B,2,H,W] f32
+ * (flow_f64 = 0) or f64 (flow_f64 = 1, added in float64 as fw.py:31); depth
+ * [B,1,H,W] f32 (depth_f64 = 0) or f64.  Output [B,Cobj+3,H,W], valid /
+ * collision [B,1,H,W] f32, bit-identical to ofd_fw_forward_warp_flow_* on the
+ * materialised obj_all (cast to float32, fw.py:40).  TILE engine only:
+ * (Cobj+3)*H*W < 2^30 (OFD_FW_ETOOBIG). */
+int ofd_fw_warp_flow_cat(const float *obj, int64_t Cobj, const void *flow, int flow_f64, const void *depth,
+                         int depth_f64, float *output, float *valid, float *collision, int64_t B, int64_t H,
+                         int64_t W, void *workspace, size_t workspace_bytes, void *stream);
 
 #ifdef __cplusplus
 }

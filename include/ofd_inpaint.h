@@ -1,5 +1,6 @@
 /*
- * ofd_inpaint.h -- C ABI of the MI355X hole-fill (layered Telea inpainting).
+ * ofd_inpaint.h -- C ABI of the MI355X hole-fill (Telea inpainting: cv2's sequential
+ * order, the default, and the faster layered order).
  *
  * Same conventions as ofd_fw.h: plain pointers and sizes, gfx950 device
  * pointers, dense contiguous NCHW float32, asynchronous on `stream` (a
@@ -93,6 +94,15 @@ int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float 
  * defaults (launches sized from an earlier call's depth; thin_cap 4096).
  * Process-wide; returns 0. */
 int ofd_inpaint_set_schedule(int launch_layers, int thin_cap);
+
+/* Test / debug hook: the OR of the invariant-violation bits any hole-fill
+ * kernel raised since the last reset -- 1: a layered tail-kernel wait gave up;
+ * 2: a sequential-march bucket index passed its bound; 4: a sequential
+ * distance sweep passed its iteration bound.  Each is unreachable while the
+ * algorithm's invariants hold, and each means that call's output is
+ * incomplete.  Blocking (a device-to-host copy of the fault words); reset != 0
+ * clears them.  Returns the bits (>= 0) or -1 on a HIP error. */
+int ofd_inpaint_faults(int reset);
 
 #ifdef __cplusplus
 }

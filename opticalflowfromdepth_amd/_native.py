@@ -33,6 +33,7 @@ SIGNATURES = {
     "ofd_fw_strerror": ([ctypes.c_int], ctypes.c_char_p),
     "ofd_fw_set_engine": ([ctypes.c_int], ctypes.c_int),
     "ofd_fw_set_disparity_rows": ([ctypes.c_int], ctypes.c_int),
+    "ofd_fw_set_row_path": ([ctypes.c_int], ctypes.c_int),
     "ofd_fw_set_profile_events": ([_P, _P], ctypes.c_int),
     "ofd_fw_workspace_bytes": ([_I64, _I64, _I64, ctypes.c_int], _SZ),
     "ofd_fw_workspace_init": ([_P, _SZ, _P], ctypes.c_int),
@@ -47,11 +48,14 @@ SIGNATURES = {
     "ofd_fw_ego_flow_f64depth": ([_P] * 4 + [_I64] * 3 + [_P], ctypes.c_int),
     "ofd_fw_warp_ego_f32": ([_P, _I64] + [_P] * 6 + [_I64] * 3 + [_P, _SZ, _P], ctypes.c_int),
     "ofd_fw_warp_ego_f64depth": ([_P, _I64] + [_P] * 6 + [_I64] * 3 + [_P, _SZ, _P], ctypes.c_int),
+    "ofd_fw_warp_flow_cat": ([_P, _I64, _P, ctypes.c_int, _P, ctypes.c_int] + [_P] * 3 + [_I64] * 3 + [_P, _SZ, _P],
+                             ctypes.c_int),
     "ofd_inpaint_workspace_bytes": ([_I64, _I64, _I64], _SZ),
     "ofd_inpaint_telea_f32": ([_P] * 4 + [_I64] * 4 + [ctypes.c_int, _P, _SZ, _P], ctypes.c_int),
     "ofd_inpaint_seq_workspace_bytes": ([_I64, _I64, _I64], _SZ),
     "ofd_inpaint_telea_seq_f32": ([_P] * 4 + [_I64] * 4 + [ctypes.c_int, _P, _SZ, _P], ctypes.c_int),
     "ofd_inpaint_set_schedule": ([ctypes.c_int, ctypes.c_int], ctypes.c_int),
+    "ofd_inpaint_faults": ([ctypes.c_int], ctypes.c_int),
 }
 
 

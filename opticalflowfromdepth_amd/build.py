@@ -1,8 +1,10 @@
 """In-tree build of the native forward-warp library for gfx950.
 
 ``python -m opticalflowfromdepth_amd.build`` or ``build_native()`` compiles
-csrc/ofd_fw.hip (forward warp) and csrc/ofd_inpaint.hip (hole-fill) with hipcc
-into ``_build/libofd_fw.so`` (C ABI, include/ofd_fw.h and include/ofd_inpaint.h).
+csrc/ofd_fw.hip (forward warp), csrc/ofd_inpaint.hip (layered hole-fill) and
+csrc/ofd_inpaint_seq.hip (the default hole-fill, cv2's sequential Telea order)
+with hipcc into ``_build/libofd_fw.so`` (C ABI, include/ofd_fw.h and
+include/ofd_inpaint.h).
 The .so is git-ignored but travels with the repo snapshot to the GPU box.
 """
 from __future__ import annotations

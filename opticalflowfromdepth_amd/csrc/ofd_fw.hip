@@ -50,6 +50,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <mutex>
 #include <type_traits>
 #include <unordered_map>
@@ -182,8 +183,14 @@ __device__ __forceinline__ void load4(const T *__restrict__ q, T v[4], int n) {
     TARGET_RANGE_EXACT
 
 // Coordinate sources: the target of the source at pixel p = j*W + i of image b.
+//
+// kRowPath: the source can take the ROW path of the persistent SPLAT (row_item
+// below).  BIN checks, per image, that every source lands, and lands in its own
+// row (ty == j, as every disparity flow does: preprocess.py:249-254); such an
+// image needs only the x coordinate (load4x / target_x) to place its sources.
 struct SafeF32 {  // fw_cuda.forward_warping inputs: safe_y, safe_x [B,1,H,W]
     using V = float;
+    static constexpr bool kRowPath = true;
     const float *sy, *sx;
     int64_t HW;
     __device__ __forceinline__ void load(int64_t b, int64_t p, V &x, V &y) const {
@@ -195,16 +202,23 @@ struct SafeF32 {  // fw_cuda.forward_warping inputs: safe_y, safe_x [B,1,H,W]
         ::load4<kVec>(sx + b * HW + p, x, n);
         ::load4<kVec>(sy + b * HW + p, y, n);
     }
+    template <bool kVec>
+    __device__ __forceinline__ void load4x(int64_t b, int64_t p, V x[4], int n) const {
+        ::load4<kVec>(sx + b * HW + p, x, n);
+    }
     __host__ bool vec_ok() const { return (uintptr_t(sx) | uintptr_t(sy)) % 16 == 0; }
     __device__ __forceinline__ void target(int64_t, int, int, V x, V y, int H, int W, int &tx, int &ty) const {
         target_safe<float>(x, y, H, W, tx, ty);
     }
+    // target column of a source BIN has proven to land in its own row
+    __device__ __forceinline__ int target_x(int, V x, int) const { return int(x); }
     KEY_DEPTH_FROM_PLANE
 };
 
 template <typename F>
 struct FlowCoords {  // FW.forward input: flow [B,2,H,W], ch0 = x, ch1 = y
     using V = F;
+    static constexpr bool kRowPath = true;
     const F *flow;
     int64_t HW;
     __device__ __forceinline__ void load(int64_t b, int64_t p, V &x, V &y) const {
@@ -218,9 +232,20 @@ struct FlowCoords {  // FW.forward input: flow [B,2,H,W], ch0 = x, ch1 = y
         ::load4<kVec>(f, x, n);
         ::load4<kVec>(f + HW, y, n);
     }
+    template <bool kVec>
+    __device__ __forceinline__ void load4x(int64_t b, int64_t p, V x[4], int n) const {
+        ::load4<kVec>(flow + b * 2 * HW + p, x, n);
+    }
     __host__ bool vec_ok() const { return uintptr_t(flow) % 16 == 0; }
     __device__ __forceinline__ void target(int64_t, int i, int j, V x, V y, int H, int W, int &tx, int &ty) const {
         target_flow<F>(i, j, x, y, H, W, tx, ty);
+    }
+    // the x half of target_flow for a source BIN has proven to land in its own
+    // row (so p0 + flow is not NaN): the same add, clamp and truncation
+    __device__ __forceinline__ int target_x(int i, V x, int W) const {
+        F px = F(i) + x;
+        px = px < F(0) ? F(0) : (px > F(W - 1) ? F(W - 1) : px);
+        return int(px);
     }
     KEY_DEPTH_FROM_PLANE
 };
@@ -236,6 +261,7 @@ template <typename D>
 struct DisparityCoords {
     using V = D;
     static constexpr int kGen = 3, kGenGT = 8;
+    static constexpr bool kRowPath = false;  // has its own row kernel (disp_row_kernel)
     const D *depth;
     const float *s;  // [B] per-image scale
     int64_t HW;
@@ -370,6 +396,7 @@ struct EgoCoords {
     // sources has been issued, which keeps SPLAT's loads in flight together.
     using V = D;
     static constexpr int kGen = 3, kGenGT = 4;
+    static constexpr bool kRowPath = false;
     const D *depth;
     const float *P;  // [B][3][4] float32 (K @ T)[:3]
     EgoCam cam;
@@ -441,6 +468,65 @@ struct EgoCoords {
             ty1 = ty0;
         }
     }
+};
+
+// FW on a flow plane the caller already holds, with obj's depth and flow
+// channels generated instead of concatenated (preprocess.py:371-373, :385-387,
+// :400-402, :414-417 all call FW(cat(img, depth, flow * -1.0[, mask]), flow,
+// depth)): the flow plane is read for the targets, the winner's depth is the
+// key's high half, its flow * -1.0 is gathered from the same plane, and the
+// concatenation is never stored.  F: the flow's dtype (float64 flows add in
+// float64, fw.py:31); D: the depth's.  The torch.cat promotes the obj to the
+// widest dtype, then fw.py:40 casts it to float32: generated channel values
+// are float32(depth) and float32(flow * -1.0), exactly those casts.
+template <typename F, typename D>
+struct FlowCatCoords {
+    using V = F;
+    static constexpr int kGen = 3, kGenGT = 8;
+    static constexpr bool kRowPath = false;
+    const F *flow;   // [B,2,H,W]
+    const D *depth;  // [B,1,H,W]
+    int64_t HW;
+    __device__ __forceinline__ void load(int64_t b, int64_t p, V &x, V &y) const {
+        const F *f = flow + b * 2 * HW + p;
+        x = f[0];
+        y = f[HW];
+    }
+    template <bool kVec>
+    __device__ __forceinline__ void load4(int64_t b, int64_t p, V x[4], V y[4], int n) const {
+        const F *f = flow + b * 2 * HW + p;
+        ::load4<kVec>(f, x, n);
+        ::load4<kVec>(f + HW, y, n);
+    }
+    template <bool kVec>
+    __device__ __forceinline__ void load4d(int64_t b, int64_t p, V x[4], V y[4], float dk[4], int n,
+                                           const float *) const {
+        load4<kVec>(b, p, x, y, n);
+        D d[4];
+        ::load4<kVec>(depth + b * HW + p, d, n);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dk[e] = float(d[e]);
+    }
+    __device__ __forceinline__ float key_depth(int64_t b, int64_t p, const float *) const {
+        return float(depth[b * HW + p]);
+    }
+    // the winner's float32 depth: the key's high half (a decoded 0 may have
+    // been -0: re-read)
+    __device__ __forceinline__ float winner_depth32(int64_t b, unsigned w, unsigned long long key) const {
+        const float d = depth_from_key(key);
+        return d != 0.0f ? d : float(depth[b * HW + w]);
+    }
+    __device__ __forceinline__ void gen_key(int64_t b, unsigned w, unsigned long long key, float g[3]) const {
+        const F *f = flow + b * 2 * HW + w;
+        g[0] = winner_depth32(b, w, key);
+        g[1] = float(f[0] * F(-1.0));
+        g[2] = float(f[HW] * F(-1.0));
+    }
+    __host__ bool vec_ok() const { return (uintptr_t(flow) | uintptr_t(depth)) % 16 == 0; }
+    __device__ __forceinline__ void target(int64_t, int i, int j, V x, V y, int H, int W, int &tx, int &ty) const {
+        target_flow<F>(i, j, x, y, H, W, tx, ty);
+    }
+    TARGET_RANGE_EXACT
 };
 
 // The ego-motion flow plane itself ([B,2,H,W] float32), four pixels of a row
@@ -550,6 +636,7 @@ struct Ws {  // views of one chunk's workspace (G images)
     ushort4 *segrec;           // [G][nseg]    scratch: target tile box (t0x,t1x,t0y,t1y) of a segment
     ushort4 *blkrec;           // [G][nsb]     scratch: same per source block
     unsigned int *queue;       // [16]         persistent SPLAT: 8 per-XCD tile queues + exit count, ~0 between calls
+    unsigned int *rowflag;     // [G]          == the chunk's epoch: image not row-local (BIN), else row path
 };
 
 inline Ws carve(void *ws, int64_t G, int64_t HW, const TileGeom &g) {
@@ -566,6 +653,7 @@ inline Ws carve(void *ws, int64_t G, int64_t HW, const TileGeom &g) {
     w.blkrec = reinterpret_cast<ushort4 *>(p);
     p += align16(size_t(G) * g.nsb * 8);
     w.queue = reinterpret_cast<unsigned int *>(p);
+    w.rowflag = w.queue + 16;  // 64 + 4 G bytes of the 256 G bytes of per-image slack
     return w;
 }
 
@@ -615,6 +703,13 @@ struct ChunkArgs {  // one chunk of images
     Ws ws;
     int64_t b0;     // first image of the chunk
     int nimg;       // images in the chunk
+    // Row path (Coords::kRowPath, fused TILE engine): 0 = off; otherwise this
+    // chunk's epoch (never 0 or ~0).  BIN stores it into ws.rowflag[image] for
+    // every image with a source that does not land in its own row; SPLAT serves
+    // the other images by rows.  A flag left from an earlier call (a repeated
+    // epoch: graph replay, wrap-around) can only send a row-local image down
+    // the general tile path, which is always correct.
+    unsigned epoch;
 };
 
 // ---- BIN: wave w of workgroup blockIdx.x boxes segment blockIdx.x * kWaves + w.
@@ -650,13 +745,17 @@ __device__ __forceinline__ void bin_segment(const Coords &co, const float *__res
     const int i0 = sgx * (SEGB * SBW) + (lane & 31) * 4;
     const int jh = sby * SBH + (lane >> 5);
     unsigned mn = 0xFFFFFFFFu, mxi = 0xFFFFFFFFu;
+    bool off_row = false;  // a source of this lane is dropped or leaves its row (row path check)
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
         const int j = jh + 2 * q;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             int tx0 = -1, tx1 = -1, ty0 = -1, ty1 = -1;
-            if (i0 + e < W && j < H) co.target_range(b, i0 + e, j, x[q][e], y[q][e], H, W, tx0, tx1, ty0, ty1);
+            if (i0 + e < W && j < H) {
+                co.target_range(b, i0 + e, j, x[q][e], y[q][e], H, W, tx0, tx1, ty0, ty1);
+                if constexpr (Coords::kRowPath) off_row |= (tx0 < 0) | (ty0 != j) | (ty1 != j);
+            }
             if (tx0 >= 0) {
                 mn = pk_min_u16(mn, unsigned(tx0 / TW) | (unsigned(ty0 / TH) << 16));
                 mxi = pk_min_u16(mxi, (0xFFFFu - unsigned(tx1 / TW)) | ((0xFFFFu - unsigned(ty1 / TH)) << 16));
@@ -690,6 +789,13 @@ __device__ __forceinline__ void bin_segment(const Coords &co, const float *__res
                                             (unsigned short)(smn >> 16), (unsigned short)(0xFFFFu - (smx >> 16)));
     // wide blocks as a bit mask over k (bit 4k of the ballot of lanes < 32)
     const unsigned long long wb = __ballot(is_wide && lane < 32 && (lane & 3) == 0);
+    // Row path: an image keeps it only if every source lands in its own row
+    // and no block spills to the key slab (the row path never merges the
+    // slab).  Every offending wave stores the same word: plain stores, no
+    // atomics; SPLAT reads it after the kernel boundary.
+    if constexpr (Coords::kRowPath) {
+        if (a.epoch != 0u && (wb != 0ull || __ballot(off_row) != 0ull) && lane == 0) ws.rowflag[bl] = a.epoch;
+    }
     if (wb == 0ull) return;  // wave-uniform
     // non-smooth flow (rare): the wide blocks' sources go to the key slab by
     // global atomic min and flag their target tiles for SPLAT's merge
@@ -891,15 +997,13 @@ __device__ __forceinline__ unsigned dequeue_tile(unsigned *queue, unsigned home,
 // Every barrier is LDS-only: global loads are consumed by the thread that
 // issued them, and the published stores are never waited for.
 template <typename Coords, bool kVec, bool kFuse, bool kStamp, typename Cfg, typename E = float>
-__device__ __forceinline__ void splat_tile(TileLds &L, unsigned lin, const Coords &co, const float *__restrict__ depth,
-                                           const SplatIO &io, const ChunkArgs &a, int H, int W, int64_t HW,
-                                           const TileGeom &g, unsigned long long *stamps) {
+__device__ __forceinline__ void splat_tile(TileLds &L, unsigned lin, int bl, int tile, const Coords &co,
+                                           const float *__restrict__ depth, const SplatIO &io, const ChunkArgs &a,
+                                           int H, int W, int64_t HW, const TileGeom &g, unsigned long long *stamps) {
     unsigned long long *ph = kStamp ? stamps + 8 * lin : nullptr;
     if constexpr (kStamp) { if (threadIdx.x == 0) ph[0] = wall_clock64(); }
 
     const Ws &ws = a.ws;
-    int bl, tile;
-    tile_of<Cfg>(lin, a, g, bl, tile);
     const unsigned fid = unsigned(bl) * unsigned(g.ntiles) + unsigned(tile);  // flag slot
     const int tyi = tile / g.tilesX, txi = tile - tyi * g.tilesX;
     const int x0 = txi * TW, y0 = tyi * TH;
@@ -1160,6 +1264,124 @@ __device__ __forceinline__ void splat_tile(TileLds &L, unsigned lin, const Coord
     }
 }
 
+// ---- ROW path (persistent SPLAT, images BIN found row-local).  Every source
+// of such an image lands in its own row, so the tile machinery (segment and
+// block scans, the re-read of every source block a tile's box touches, the key
+// slab) is not needed: item `tile` of the image covers the rows
+// [tile*H/ntiles, (tile+1)*H/ntiles) -- about the rows of the tile row band
+// the index maps to -- in sub-bands of TW*TH/W rows, each folded into the LDS
+// z-buffer (the same lexmin keys) and published with 16-byte loads and stores.
+// Sources are read once (x coordinate and depth; the y coordinate is not
+// needed once BIN has shown ty == j), the winners' obj channels come from the
+// same rows.  The host enables it only with W <= TW*TH, W % 4 == 0 and every
+// plane 16-byte aligned (8-byte for bf16 planes).
+typedef float RowV4F __attribute__((ext_vector_type(4)));
+typedef unsigned short RowV4H __attribute__((ext_vector_type(4)));
+
+template <typename E>
+__device__ __forceinline__ void put4_nt(E *dst, const E v[4]) {
+    if constexpr (sizeof(E) == 4)
+        __builtin_nontemporal_store(RowV4F{v[0], v[1], v[2], v[3]}, reinterpret_cast<RowV4F *>(dst));
+    else
+        __builtin_nontemporal_store(RowV4H{v[0], v[1], v[2], v[3]}, reinterpret_cast<RowV4H *>(dst));
+}
+
+constexpr int kRowQ = 2;  // quads (4 targets) per thread in flight: fold
+constexpr int kRowQP = 1;  // publish
+
+template <typename Coords, typename Cfg, typename E>
+__device__ __forceinline__ void row_item(TileLds &L, int bl, int tile, const Coords &co, const float *__restrict__ depth,
+                                         const SplatIO &io, const ChunkArgs &a, int H, int W, int64_t HW,
+                                         const TileGeom &g) {
+    using V = typename Coords::V;
+    const int64_t b = a.b0 + bl;
+    const int r0 = int(int64_t(tile) * H / g.ntiles), r1 = int(int64_t(tile + 1) * H / g.ntiles);
+    const int RB = (TW * TH) / W;  // rows per sub-band (>= 1)
+    const int qpr = W >> 2;        // quads per row
+    const int C = io.C;
+    const E *ob = static_cast<const E *>(io.obj) + b * int64_t(io.Cobj) * HW;
+    E *oo = static_cast<E *>(io.out) + b * int64_t(C) * HW;
+    float *vb = io.valid + b * HW;
+    float *cb = io.coll + b * HW;
+    const unsigned uHW = unsigned(HW);
+    for (int ra = r0; ra < r1; ra += RB) {
+        const int rb = ra + RB < r1 ? ra + RB : r1;
+        const int n = (rb - ra) * W, nq = n >> 2;
+        const unsigned base = unsigned(ra) * unsigned(W);  // image-local index of the sub-band's first pixel
+        for (int k = threadIdx.x; k < n; k += Cfg::kThr) L.zk[k] = KEY_UNTOUCHED;
+        lds_barrier();
+        // fold: kRowQ quads per thread, every load issued before the first key
+        for (int q0 = threadIdx.x; q0 < nq; q0 += Cfg::kThr * kRowQ) {
+            V x[kRowQ][4];
+            float d[kRowQ][4];
+#pragma unroll
+            for (int u = 0; u < kRowQ; ++u) {
+                const int q = q0 + u * Cfg::kThr;
+                if (q < nq) {
+                    co.template load4x<true>(b, int64_t(base) + 4 * q, x[u], 4);
+                    ::load4<true>(depth + b * HW + base + 4 * q, d[u], 4);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kRowQ; ++u) {
+                const int q = q0 + u * Cfg::kThr;
+                if (q >= nq) break;
+                const int lr = q / qpr, i0 = (q - lr * qpr) * 4;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int tx = co.target_x(i0 + e, x[u][e], W);
+                    atomicMin(&L.zk[lr * W + tx], make_key(d[u][e], base + unsigned(4 * q + e)));
+                }
+            }
+        }
+        lds_barrier();
+        // publish: valid, collision, and the winners' C channels
+        for (int q0 = threadIdx.x; q0 < nq; q0 += Cfg::kThr * kRowQP) {
+            unsigned w[kRowQP][4];
+#pragma unroll
+            for (int u = 0; u < kRowQP; ++u) {
+                const int q = q0 + u * Cfg::kThr;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) w[u][e] = WIN_NONE;
+                if (q >= nq) break;
+                float vv[4], cv[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const unsigned long long key = L.zk[4 * q + e];
+                    const bool touched = key != KEY_UNTOUCHED, nowin = key == KEY_NOWIN;
+                    w[u][e] = (touched && !nowin) ? unsigned(key & 0xFFFFFFFFull) : WIN_NONE;
+                    vv[e] = touched ? 1.f : 0.f;
+                    cv[e] = nowin ? 1.f : 0.f;
+                }
+                put4_nt<float>(vb + base + 4 * q, vv);
+                put4_nt<float>(cb + base + 4 * q, cv);
+            }
+            constexpr int kCh = 4;
+            for (int c0 = 0; c0 < C; c0 += kCh) {
+                E o[kRowQP][kCh][4];
+#pragma unroll
+                for (int u = 0; u < kRowQP; ++u)
+#pragma unroll
+                    for (int cc = 0; cc < kCh; ++cc)
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            o[u][cc][e] = (q0 + u * Cfg::kThr < nq && c0 + cc < C && w[u][e] != WIN_NONE)
+                                              ? ob[unsigned(c0 + cc) * uHW + w[u][e]]
+                                              : E(0);
+#pragma unroll
+                for (int u = 0; u < kRowQP; ++u) {
+                    const int q = q0 + u * Cfg::kThr;
+                    if (q >= nq) break;
+#pragma unroll
+                    for (int cc = 0; cc < kCh; ++cc)
+                        if (c0 + cc < C) put4_nt<E>(oo + unsigned(c0 + cc) * uHW + base + 4 * q, o[u][cc]);
+                }
+            }
+        }
+        if (ra + RB < r1) lds_barrier();  // the next sub-band re-initialises the z-buffer
+    }
+}
+
 using SplitCfg = SplatCfg<512, 2, 8>;  // split engine: 4 workgroups / CU, light publish
 // fused engine: 2 workgroups / CU (VGPR-bound), every target's gathers of a
 // thread (8 x C) in flight at once.  Measured at 64 x 768x1024, C = 6
@@ -1188,7 +1410,9 @@ __global__ __launch_bounds__(Cfg::kThr, Cfg::kMinW) void splat_kernel(Coords co,
     const unsigned per = (total + 7u) / 8u;
     const unsigned lin = (blockIdx.x % 8u) * per + blockIdx.x / 8u;
     if (lin >= total) return;
-    splat_tile<Coords, kVec, kFuse, kStamp, Cfg>(L, lin, co, depth, io, a, H, W, HW, g, stamps);
+    int bl, tile;
+    tile_of<Cfg>(lin, a, g, bl, tile);
+    splat_tile<Coords, kVec, kFuse, kStamp, Cfg>(L, lin, bl, tile, co, depth, io, a, H, W, HW, g, stamps);
 }
 
 // Persistent SPLAT: one workgroup per resident slot, looping over tiles.  The
@@ -1216,7 +1440,15 @@ __global__ __launch_bounds__(Cfg::kThr, Cfg::kMinW) void splat_persist_kernel(Co
         lds_barrier();
         const unsigned lin = L.next;
         if (lin == ~0u) return;
-        splat_tile<Coords, kVec, kFuse, kStamp, Cfg, E>(L, lin, co, depth, io, a, H, W, HW, g, stamps);
+        int bl, tile;
+        tile_of<Cfg>(lin, a, g, bl, tile);
+        if constexpr (kFuse && kVec && Coords::kRowPath && !kStamp) {
+            if (a.epoch != 0u && a.ws.rowflag[bl] != a.epoch) {  // row-local image (BIN, previous launch)
+                row_item<Coords, Cfg, E>(L, bl, tile, co, depth, io, a, H, W, HW, g);
+                continue;
+            }
+        }
+        splat_tile<Coords, kVec, kFuse, kStamp, Cfg, E>(L, lin, bl, tile, co, depth, io, a, H, W, HW, g, stamps);
         // splat_tile ends with LDS reads of the z-buffer; the next iteration's
         // barrier orders them before the next tile's initialisation
     }
@@ -1470,6 +1702,28 @@ unsigned persist_grid(unsigned tiles) {
     return tiles < slots ? tiles : slots;
 }
 
+// Row path of the persistent SPLAT (row_item): on by default; OFD_FW_ROWPATH=0
+// or ofd_fw_set_row_path(0) turns it off (A/B and tests).
+int g_row_path = -1;
+
+bool row_path_enabled() {
+    static const bool env_on = [] {
+        const char *e = getenv("OFD_FW_ROWPATH");
+        return !(e && e[0] == '0');
+    }();
+    return g_row_path < 0 ? env_on : g_row_path != 0;
+}
+
+// A fresh chunk epoch for the row path: never 0 (off) or ~0 (the value an
+// initialised workspace holds).
+std::atomic<unsigned> g_epoch{0};
+unsigned next_epoch() {
+    for (;;) {
+        const unsigned e = g_epoch.fetch_add(1u, std::memory_order_relaxed) + 1u;
+        if (e != 0u && e != ~0u) return e;
+    }
+}
+
 // Optional timing hook (ofd_fw_set_profile_events): events recorded on the
 // launch stream right before the first and right after the last RESOLVE
 // launch of a call -- the dominant kernel -- so a benchmark can time it with
@@ -1513,10 +1767,14 @@ int run_f32(Coords co, const E *obj, const float *depth, E *out, float *valid, f
     const Ws slab = carve(ws, G, HW, g);
     // 16-byte coordinate / depth loads in BIN and SPLAT
     const bool vec = W % 4 == 0 && co.vec_ok() && uintptr_t(depth) % 16 == 0;
+    // row path: 16-byte (8-byte for bf16) output, valid and collision stores
+    const bool row_path = Coords::kRowPath && mode == Mode::Tile && vec && W <= TW * TH && row_path_enabled() &&
+                          aligned(out, 4 * sizeof(E)) && aligned(valid, 16) && aligned(coll, 16);
     for (int64_t c = 0; c < nch; ++c) {
         const int64_t b0 = c * G;
         const int64_t nb = (B - b0) < G ? (B - b0) : G;
         const int64_t px = nb * HW;
+        const unsigned epoch = row_path ? next_epoch() : 0u;
         if constexpr (!kTileOnly) {
             if (mode == Mode::Atomic) {
                 hipLaunchKernelGGL((splat_atomic_kernel<Coords>), dim3(grid_for(px, kBlock * 4)), dim3(kBlock), 0,
@@ -1529,7 +1787,7 @@ int run_f32(Coords co, const E *obj, const float *depth, E *out, float *valid, f
             }
         }
         {
-            const ChunkArgs a{slab, b0, int(nb)};
+            const ChunkArgs a{slab, b0, int(nb), epoch};
             const SplatIO io{valid, coll, obj, out, int(C), int(C) - Coords::kGen, gen_at};
             const dim3 bgrid(grid_for(nb * g.nseg, kWaves * kBinSPW));
             if (vec)
@@ -1715,6 +1973,12 @@ int ofd_fw_set_disparity_rows(int on) {
     return prev;
 }
 
+int ofd_fw_set_row_path(int on) {
+    const int prev = row_path_enabled() ? 1 : 0;
+    if (on == 0 || on == 1) g_row_path = on;
+    return prev;
+}
+
 int ofd_fw_set_engine(int engine) {
     const int prev = int(engine_mode());
     if (engine == OFD_FW_ENGINE_TILE || engine == OFD_FW_ENGINE_ATOMIC || engine == OFD_FW_ENGINE_TILE_SPLIT)
@@ -1871,6 +2135,26 @@ int warp_ego(const float *obj, int64_t Cobj, const D *depth, const float *P, con
 }  // namespace
 
 extern "C" {
+
+int ofd_fw_warp_flow_cat(const float *obj, int64_t Cobj, const void *flow, int flow_f64, const void *depth,
+                         int depth_f64, float *output, float *valid, float *collision, int64_t B, int64_t H,
+                         int64_t W, void *workspace, size_t workspace_bytes, void *stream) {
+    if (Cobj < 0) return OFD_FW_EINVAL;
+    const int64_t C = Cobj + 3;
+    if (int rc = check_dims(B, C, H, W)) return rc;
+    if (B * H * W > 0 && (!flow || !depth || !valid || !collision || !output || (Cobj > 0 && !obj)))
+        return OFD_FW_EINVAL;
+    if (!aligned(flow, flow_f64 ? 8 : 4) || !aligned(depth, depth_f64 ? 8 : 4)) return OFD_FW_EALIGN;
+    const int gen_at = int(Cobj < 3 ? Cobj : 3);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const int64_t HW = H * W;
+#define OFD_FLOW_CAT(F, D)                                                                                   \
+    run_f32(FlowCatCoords<F, D>{static_cast<const F *>(flow), static_cast<const D *>(depth), HW}, obj, nullptr, \
+            output, valid, collision, B, C, H, W, workspace, workspace_bytes, st, gen_at)
+    if (flow_f64) return depth_f64 ? OFD_FLOW_CAT(double, double) : OFD_FLOW_CAT(double, float);
+    return depth_f64 ? OFD_FLOW_CAT(float, double) : OFD_FLOW_CAT(float, float);
+#undef OFD_FLOW_CAT
+}
 
 int ofd_fw_ego_flow_f32(const float *depth, const float *P, const float *inv_K, float *flow, int64_t B, int64_t H,
                         int64_t W, void *stream) {

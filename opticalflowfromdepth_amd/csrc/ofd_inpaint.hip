@@ -56,6 +56,12 @@
 
 #pragma clang fp contract(off)
 
+// Fault word of the layered fill (ofd_inpaint_faults): bit 0 = a tail-kernel
+// wait gave up (should be unreachable, see below).
+__device__ unsigned g_ip_fault;
+
+unsigned ofd_sq_fault_read(int reset);  // ofd_inpaint_seq.hip
+
 namespace {
 
 #include "ip_common.h"
@@ -727,7 +733,8 @@ __global__ __launch_bounds__(1024) void ip_scan_kernel(const unsigned *__restric
     }
     if (tid == 0) {
         meta[0] = lmax;
-        meta[1] = 0u;  // the deep tail kernel's barrier counter
+        meta[1] = 0u;  // the deep tail kernel's ticket counter
+        meta[2] = 0u;  // ... and its finished-block counter
     }
 }
 
@@ -1137,19 +1144,22 @@ __device__ __forceinline__ void hole_wave_lds(const Chunk &ch, const uint32_t *_
 // (thread per hole, or kCS threads per hole up to kCsSplitMax holes) and the
 // rest of the grid the others (wave per hole), each part grid-stride.  The
 // two sets of a layer are independent; every block runs one path.
+// Block `bx` of a G-block partition of hole layer L (a launch's blockIdx.x /
+// gridDim.x, or the tail kernel's ticket).
 __device__ __forceinline__ void hole_layer_body(const Chunk &ch, const uint32_t *__restrict__ list,
                                                 const unsigned *__restrict__ hist, const unsigned *__restrict__ cursor,
-                                                int nring, unsigned L, int range, unsigned thin_cap, WavePatch *patch) {
+                                                int nring, unsigned L, int range, unsigned thin_cap, WavePatch *patch,
+                                                unsigned bx, unsigned G) {
     const int bi = nring + 2 * (int(L) - 1);
     const unsigned ni = hist[bi], nw = hist[bi + 1];
     if (ni + nw == 0u) return;
     // SCATTER advanced cursor[] to each bin's end: a bin starts at cursor - count
     const uint32_t *lp = list + (cursor[bi] - ni), *lw = list + (cursor[bi + 1] - nw);
-    const unsigned wave = threadIdx.x >> 6, G = gridDim.x;
-    IP_STAMP(2 * L, 0, blockIdx.x == 0 && threadIdx.x == 0);
-    IP_STAMP(2 * L + 1, 0, blockIdx.x == G - 1 && threadIdx.x == 0);
+    const unsigned wave = threadIdx.x >> 6;
+    IP_STAMP(2 * L, 0, bx == 0 && threadIdx.x == 0);
+    IP_STAMP(2 * L + 1, 0, bx == G - 1 && threadIdx.x == 0);
     if (range <= 3 && ni + nw <= thin_cap) {
-        for (unsigned h = blockIdx.x * 4u + wave; h < ni + nw; h += G * 4u) {
+        for (unsigned h = bx * 4u + wave; h < ni + nw; h += G * 4u) {
             if (h < ni)
                 hole_wave_lds(ch, lp, ni, h, L, range, patch[wave]);
             else
@@ -1162,8 +1172,8 @@ __device__ __forceinline__ void hole_layer_body(const Chunk &ch, const uint32_t 
     // split the grid in proportion to the two parts' blocks (each part at least one block)
     unsigned gb = bt + bw <= G ? bt : (bw == 0u ? G : (bt == 0u ? 0u : max(1u, unsigned(uint64_t(G) * bt / (bt + bw)))));
     if (bw && gb >= G) gb = G - 1u;
-    if (blockIdx.x < gb) {
-        for (unsigned i = blockIdx.x * 256u + threadIdx.x; i < ni * cs; i += gb * 256u) {
+    if (bx < gb) {
+        for (unsigned i = bx * 256u + threadIdx.x; i < ni * cs; i += gb * 256u) {
             if (cs == 1u)
                 hole_patch<1>(ch, lp, ni, i, L);
             else
@@ -1171,7 +1181,7 @@ __device__ __forceinline__ void hole_layer_body(const Chunk &ch, const uint32_t 
         }
     } else {
         const unsigned gw = G - gb;
-        for (unsigned h = (blockIdx.x - gb) * 4u + wave; h < nw; h += gw * 4u) {
+        for (unsigned h = (bx - gb) * 4u + wave; h < nw; h += gw * 4u) {
             if (range <= 3)
                 hole_wave_lds(ch, lw, nw, h, L, range, patch[wave]);
             else
@@ -1186,46 +1196,62 @@ __global__ __launch_bounds__(256) void ip_hole_layer_kernel(Chunk ch, const uint
                                                             const unsigned *__restrict__ cursor, int nring, unsigned L,
                                                             int range, unsigned thin_cap) {
     __shared__ WavePatch patch[4];
-    hole_layer_body(ch, list, hist, cursor, nring, L, range, thin_cap, patch);
-}
-
-// Grid barrier of the deep tail kernel (every workgroup resident): a
-// monotonic arrival counter, lane 0 of each workgroup releasing its stores at
-// agent scope before arriving and acquiring after the last arrival
-// (MI355X_MICROARCH.md, inter-workgroup visibility).
-__device__ __forceinline__ void tail_grid_sync(unsigned *count, unsigned nblocks, unsigned &gen) {
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned target = (++gen) * nblocks;
-        __hip_atomic_fetch_add(count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // bounded: a workgroup that never arrives (it cannot happen with one
-        // resident workgroup per CU) ends the wait instead of hanging the GPU
-        for (unsigned spin = 0; spin < (1u << 26) &&
-                                __hip_atomic_load(count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target;
-             ++spin)
-            __builtin_amdgcn_s_sleep(2);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
+    hole_layer_body(ch, list, hist, cursor, nring, L, range, thin_cap, patch, blockIdx.x, gridDim.x);
 }
 
 // The layers beyond the ones the host launched (L0 .. meta[0], the deepest
-// layer the sort found): one persistent launch, a grid barrier between
-// layers.  Exits at once when meta[0] < L0 (the usual case: the host sizes
-// its launches from the previous call's depth).
+// layer the sort found), as a ticket queue that needs NO co-residency:
+// ticket t is block t % G of layer L0 + t / G (the partition a G-block layer
+// launch would use).  A workgroup takes a ticket (meta[1]), waits until every
+// block of the earlier tail layers has finished (meta[2] >= (t / G) * G),
+// runs its block, releases its stores and counts it done.  Tickets are handed
+// out in order, so every block a ticket waits for was taken earlier by a
+// workgroup that is running and waits only on still earlier tickets: the queue
+// drains whatever number of workgroups is resident (other streams' kernels may
+// hold CUs).  Exits at once when meta[0] < L0 (the usual case: the host sizes
+// its launches from the previous calls' depth).  meta[1], meta[2] are zeroed
+// by ip_scan_kernel before every call's tail.
 __global__ __launch_bounds__(256) void ip_hole_tail_kernel(Chunk ch, const uint32_t *__restrict__ list,
                                                            const unsigned *__restrict__ hist,
                                                            const unsigned *__restrict__ cursor, unsigned *meta,
                                                            int nring, unsigned L0, int range, unsigned thin_cap) {
     __shared__ WavePatch patch[4];
+    __shared__ unsigned s_ticket;
     const unsigned lmax = meta[0];
-    unsigned gen = 0;
-    for (unsigned L = L0; L <= lmax; ++L) {
-        hole_layer_body(ch, list, hist, cursor, nring, L, range, thin_cap, patch);
-        if (L < lmax) tail_grid_sync(meta + 1, gridDim.x, gen);
+    if (lmax < L0) return;
+    const unsigned G = gridDim.x, total = (lmax - L0 + 1u) * G;
+    for (;;) {
+        if (threadIdx.x == 0) {
+            const unsigned t = __hip_atomic_fetch_add(meta + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (t < total) {
+                const unsigned need = (t / G) * G;
+                // bounded (~seconds): the wait is on running workgroups only,
+                // so it ends; a give-up is recorded, never silent
+                unsigned spin = 0;
+                while (__hip_atomic_load(meta + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+                    __builtin_amdgcn_s_sleep(2);
+                    if (++spin == (1u << 28)) {
+                        atomicOr(&g_ip_fault, 1u);
+                        break;
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            s_ticket = t;
+        }
+        __syncthreads();
+        const unsigned t = s_ticket;
+        if (t >= total) return;
+        hole_layer_body(ch, list, hist, cursor, nring, L0 + t / G, range, thin_cap, patch, t % G, G);
+        // publish the block: every wave's stores drained, then one release + count
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_fetch_add(meta + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 
@@ -1260,8 +1286,8 @@ unsigned default_layer_grid() {
     return v;
 }
 
-// The deep tail kernel's grid barrier needs every workgroup resident: one
-// 256-thread workgroup per CU (its registers and LDS admit two).
+// The deep tail kernel's grid: one 256-thread workgroup per CU (its tickets
+// do not need them resident together).
 unsigned tail_grid() {
     static const unsigned v = [] {
         int dev = 0, cus = 0;
@@ -1355,6 +1381,18 @@ LaggedStats &lagged_stats(int64_t nb, int64_t H, int64_t W, int r) {
 }  // namespace
 
 extern "C" {
+
+int ofd_inpaint_faults(int reset) {
+    unsigned v = 0;
+    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_ip_fault), sizeof(v)) != hipSuccess) return -1;
+    if (reset) {
+        const unsigned z = 0;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_ip_fault), &z, sizeof(z)) != hipSuccess) return -1;
+    }
+    const unsigned q = ofd_sq_fault_read(reset);
+    if (q == ~0u) return -1;
+    return int((v & 1u) | (q & 6u));
+}
 
 int ofd_inpaint_set_schedule(int launch_layers, int thin_cap) {
     g_launch_layers = launch_layers < 0 ? -1 : launch_layers;

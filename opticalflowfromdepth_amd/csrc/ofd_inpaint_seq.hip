@@ -58,6 +58,12 @@
 
 #pragma clang fp contract(off)
 
+// Fault bits of the sequential fill (ofd_inpaint_faults): 2 = a march bucket
+// index past its bound, 4 = a distance sweep past its iteration bound (both
+// unreachable while the margin argument holds; the kernel stops early and the
+// output is incomplete, so a set bit means a wrong result).
+__device__ unsigned g_sq_fault;
+
 namespace {
 
 #include "ip_common.h"
@@ -632,7 +638,7 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
             if (lo == seq) break;  // nothing pending in buckets >= k
         }
         if (k > 4u * uint32_t(m.en) + 16u) {  // cannot happen: bucket k holds T >= k w >= k / 2 and T < en
-            if (tid == 0) m.meta[5] = 1u;
+            if (tid == 0) { m.meta[5] = 1u; atomicOr(&g_sq_fault, 2u); }
             break;
         }
         start[k & 3] = seq;
@@ -820,7 +826,7 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
             __syncthreads();
             for (uint32_t it = 0;; ++it) {
                 if (it > npush + 1) {
-                    if (tid == 0) m.meta[5] = 2u;
+                    if (tid == 0) { m.meta[5] = 2u; atomicOr(&g_sq_fault, 4u); }
                     break;
                 }
                 if (tid == 0) L.chg = 0u;
@@ -889,7 +895,7 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
             uint32_t nw = npush;
             for (uint32_t it = 0;; ++it) {
                 if (it > npush + 1) {
-                    if (tid == 0) m.meta[5] = 2u;
+                    if (tid == 0) { m.meta[5] = 2u; atomicOr(&g_sq_fault, 4u); }
                     break;
                 }
                 if (tid == 0) L.chg = 0u;
@@ -1794,6 +1800,16 @@ __global__ __launch_bounds__(256) void sq_unpack_kernel(SqWs w, float *__restric
 
 }  // namespace
 
+unsigned ofd_sq_fault_read(int reset) {
+    unsigned v = 0;
+    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_sq_fault), sizeof(v)) != hipSuccess) return ~0u;
+    if (reset) {
+        const unsigned z = 0;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_sq_fault), &z, sizeof(z)) != hipSuccess) return ~0u;
+    }
+    return v;
+}
+
 extern "C" {
 
 size_t ofd_inpaint_seq_workspace_bytes(int64_t B, int64_t H, int64_t W) {
@@ -1810,6 +1826,10 @@ int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float 
     if (H < 2 || W < 2) return OFD_FW_EINVAL;
     const int64_t en = (H + 2) * (W + 2);
     if (en >= (int64_t(1) << 30)) return OFD_FW_ETOOBIG;  // ranks * 4 + direction fit 32 bits
+    // the buckets' margin (a push lands >= 1/sqrt(2) above its popper, the
+    // bucket is <= 0.7 wide) needs the float rounding of T well under 0.2:
+    // T < H + W < 2^19 keeps its ulp at or below 2^-5
+    if (H + W >= (int64_t(1) << 19)) return OFD_FW_ETOOBIG;
     const int r = radius < 1 ? 1 : (radius > kMaxRange ? kMaxRange : radius);
     if (!workspace || (reinterpret_cast<uintptr_t>(workspace) & 255u)) return OFD_FW_EWORKSPACE;
     const size_t pi = per_image_bytes(H, W), fixed = 8 * 256;

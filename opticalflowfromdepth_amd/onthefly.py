@@ -108,10 +108,9 @@ def make_pairs(rgb, raw_depth, s, T, kind, ops: PairOps = PairOps(), dtype=torch
     image1 = rgb.to(dtype).contiguous()
     out, warped_valid, coll = ops.warp(image1, flow, depth.contiguous())
     image2 = ops.fill((out.to(torch.float32) * warped_valid), warped_valid, coll).to(dtype)
-    ys, xs = torch.meshgrid(torch.arange(H, device=rgb.device, dtype=torch.float32),
-                            torch.arange(W, device=rgb.device, dtype=torch.float32), indexing="ij")
-    tx, ty = xs + flow[:, 0], ys + flow[:, 1]
-    valid = ((tx >= 0) & (tx <= W - 1) & (ty >= 0) & (ty <= H - 1)).to(torch.float32)
+    # the reference training data's supervision mask (adjusted_RAFT/core/datasets.py:282-288):
+    # flow components under 1000 px, and no sky / invalid depth (normalize_depth's sentinel 100)
+    valid = ((flow[:, 0].abs() < 1000) & (flow[:, 1].abs() < 1000) & (depth[:, 0] != 100)).to(torch.float32)
     return image1, image2, flow, valid
 
 

@@ -13,7 +13,9 @@ the warp (preprocess.py:356-359 / :371-373, :385-387); ``ego_flow`` is the
 ego-motion flow plane alone (preprocess.py:265-298).
 
 ``inpaint`` is the batched hole-fill that replaces ``utils.inpaint``
-(utils.py:136-151) with the layered Telea kernels of csrc/ofd_inpaint.hip.
+(utils.py:136-151): by default cv2's sequential Telea order run on the GPU
+(csrc/ofd_inpaint_seq.hip, ``order="sequential"``), or the faster layered
+re-specification (csrc/ofd_inpaint.hip, ``order="layered"``).
 
 Both launch asynchronously on the current HIP stream of the input's device.
 There is no CPU path: the reference raises for non-GPU tensors
@@ -194,6 +196,19 @@ def forward_warp_flow(obj: torch.Tensor, flow: torch.Tensor, depth: torch.Tensor
 
 INPAINT_ORDERS = ("sequential", "layered")
 
+# Hole-fill workspace budget per (device, stream) cache entry, in bytes
+# (OFD_INPAINT_WS_GB, default 32 GiB: 3 x 64 headline images in one chunk; at most
+# _WS_CACHE_MAX entries live).
+_INPAINT_WS_BUDGET = int(float(os.environ.get("OFD_INPAINT_WS_GB", "32")) * (1 << 30))
+
+
+def inpaint_chunk_images(ws_bytes_fn, H: int, W: int) -> int:
+    """Images per hole-fill chunk under the workspace budget (at least one)."""
+    one = int(ws_bytes_fn(1, H, W))
+    two = int(ws_bytes_fn(2, H, W))
+    per = max(two - one, 1)
+    return max(1, (_INPAINT_WS_BUDGET - (one - per)) // per)
+
 
 def default_inpaint_order() -> str:
     """The hole-fill order ops.inpaint uses when none is given: OFD_INPAINT_ORDER, else "sequential"."""
@@ -255,7 +270,11 @@ def inpaint(img: torch.Tensor, valid: torch.Tensor, collision: torch.Tensor, rad
         collision = collision.to(_F32).contiguous()
         out = torch.empty_like(img)
         lib = _native.lib()
-        nbytes = int((lib.ofd_inpaint_seq_workspace_bytes if seq else lib.ofd_inpaint_workspace_bytes)(B, H, W))
+        wsb = lib.ofd_inpaint_seq_workspace_bytes if seq else lib.ofd_inpaint_workspace_bytes
+        # the library fills the batch in chunks of as many images as the
+        # workspace holds: cap it at a byte budget (~210 B per padded pixel for
+        # the sequential fill, ~32 GB for 3 x 64 headline images otherwise)
+        nbytes = int(wsb(min(B, inpaint_chunk_images(wsb, H, W)), H, W))
         ws = None
         if nbytes:
             key = (dev.index, stream.cuda_stream)
@@ -402,4 +421,50 @@ def warp_ego(obj: torch.Tensor, depth: torch.Tensor, P: torch.Tensor, inv_K: tor
                 valid.data_ptr(), collision.data_ptr(), B, H, W, ws.data_ptr() if ws is not None else None,
                 ws.numel() if ws is not None else 0, stream.cuda_stream)
         _native.check(rc, "warp_ego")
+    return output, valid, collision
+
+
+def warp_flow_cat(obj: torch.Tensor, flow: torch.Tensor, depth: torch.Tensor,
+                  out: Tuple[torch.Tensor, torch.Tensor, torch.Tensor] = None
+                  ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """FW(torch.cat((obj[:, :3], depth, flow * -1.0, obj[:, 3:]), 1), flow, depth)
+    on a flow plane the caller holds, in one native call that never stores the
+    concatenation (include/ofd_fw.h ofd_fw_warp_flow_cat): preprocess.py:371-373,
+    :385-387 (ego-motion flows), :400-402, :414-417 (composed flows).
+    obj [B,Cobj,H,W] float32, flow [B,2,H,W] float32 / float64, depth [B,1,H,W]
+    float32 / float64.  Returns (output [B,Cobj+3,H,W], valid, collision),
+    bit-identical to forward_warp_flow on the concatenation."""
+    for x, n in ((obj, "obj"), (flow, "flow"), (depth, "depth")):
+        _check_input(x, n)
+    if obj.dim() != 4:
+        raise RuntimeError("warp_flow_cat expects obj [B,C,H,W]")
+    B, Cobj, H, W = obj.shape
+    if tuple(flow.shape) != (B, 2, H, W):
+        raise RuntimeError(f"flow must have shape {(B, 2, H, W)}, got {tuple(flow.shape)}")
+    if tuple(depth.shape) != (B, 1, H, W):
+        raise RuntimeError(f"depth must have shape {(B, 1, H, W)}, got {tuple(depth.shape)}")
+    if obj.dtype != _F32:
+        raise RuntimeError("warp_flow_cat expects a float32 obj")
+    for x, n in ((flow, "flow"), (depth, "depth")):
+        if x.dtype not in (_F32, _F64):
+            raise RuntimeError(f"{n} must be float32 or float64, got {x.dtype}")
+    dev = obj.device
+    if flow.device != dev or depth.device != dev:
+        raise RuntimeError("obj, flow and depth must be on one device")
+    with torch.cuda.device(dev):
+        stream = torch.cuda.current_stream(dev)
+        if out is None:
+            output = torch.empty(B, Cobj + 3, H, W, dtype=_F32, device=dev)
+            valid = torch.empty(B, 1, H, W, dtype=_F32, device=dev)
+            collision = torch.empty_like(valid)
+        else:
+            output, valid, collision = _check_out(out, ((B, Cobj + 3, H, W), (B, 1, H, W), (B, 1, H, W)),
+                                                  (_F32, _F32, _F32), dev)
+        nbytes = _ws_bytes(B, H, W, False)
+        ws = workspace(dev, nbytes, stream) if nbytes else None
+        rc = _native.lib().ofd_fw_warp_flow_cat(
+            obj.data_ptr(), Cobj, flow.data_ptr(), int(flow.dtype == _F64), depth.data_ptr(),
+            int(depth.dtype == _F64), output.data_ptr(), valid.data_ptr(), collision.data_ptr(), B, H, W,
+            ws.data_ptr() if ws is not None else None, ws.numel() if ws is not None else 0, stream.cuda_stream)
+        _native.check(rc, "warp_flow_cat")
     return output, valid, collision

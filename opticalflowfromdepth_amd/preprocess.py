@@ -32,7 +32,7 @@ from torch import nn
 
 from . import synth
 from .fw import FW
-from .ops import ego_flow, inpaint, warp_disparity, warp_ego
+from .ops import ego_flow, inpaint, warp_disparity, warp_flow_cat
 from .synth import fix_warped_depth, get_random, normalize_depth
 
 AUGMENT_SCHEDULE = (0, 5, 6, 7, 1, 5, 6, 7, 2, 5, 6, 7)  # preprocess.py:454
@@ -394,12 +394,13 @@ class PreprocessPlusAugment(nn.Module):
 
         # :385-387 -- independent of img1's fill, so its hole-fill shares one
         # call with img1's (the fill is per image; one launch over 2B images
-        # keeps twice the workgroups busy).  The ego-motion flow plane is
-        # kept (a group output); the fused warp derives the same flow
-        # in-kernel and generates obj's depth / flow channels.
-        P, ik = synth.projection(img0.shape[-2], img0.shape[-1], T1, img0.device)
+        # keeps twice the workgroups busy).  The ego-motion flow plane is a
+        # group output, so the warp reads it (warp_flow_cat: obj's depth and
+        # flow channels generated from the winner, the concatenation never
+        # stored) instead of deriving the flow again.
         flow03, _ = Convert.depth_to_random_flow(img0_depth, T1=T1)                    # :385
-        o, img3_valid, coll3 = warp_ego(img0.to(torch.float32).contiguous(), img0_depth.contiguous(), P, ik)
+        o, img3_valid, coll3 = warp_flow_cat(img0.to(torch.float32).contiguous(), flow03.contiguous(),
+                                             img0_depth.contiguous())
         img3, img3_depth, back_flow03 = o[:, 0:3], o[:, 3:4], o[:, 4:6]
         img3 = img3 * img3_valid
         img3_depth = img3_depth * img3_valid
@@ -413,7 +414,8 @@ class PreprocessPlusAugment(nn.Module):
         # :372-373: bit-identical to
         # fw(cat(img1, img1_depth, flow12 * -1.0, img1_valid), flow12, img1_depth)
         flow12, _ = Convert.depth_to_random_flow(img1_depth, T1=T1)                    # :372
-        o, valid, coll2 = warp_ego(torch.cat((img1, img1_valid), 1), img1_depth.contiguous(), P, ik)
+        o, valid, coll2 = warp_flow_cat(torch.cat((img1, img1_valid), 1).to(torch.float32), flow12.contiguous(),
+                                        img1_depth.contiguous())
         img2, img2_depth, back_flow12, fw_img1_valid = o[:, 0:3], o[:, 3:4], o[:, 4:6], o[:, 6:7]
         img2_valid = valid * fw_img1_valid
         img2 = img2 * img2_valid
@@ -422,7 +424,9 @@ class PreprocessPlusAugment(nn.Module):
         img2_depth = fix_warped_depth(img2_depth)
 
         flow02, flow02_valid = cf(flow01, back_flow01, flow12, img1_depth)             # :400
-        o, valid, coll2p = fw(torch.cat((img0, img0_depth, flow02 * -1.0, flow02_valid), 1), flow02, img0_depth)
+        # :401-402 (fw(cat(img0, img0_depth, flow02 * -1.0, flow02_valid), flow02, img0_depth))
+        o, valid, coll2p = warp_flow_cat(torch.cat((img0, flow02_valid), 1).to(torch.float32), flow02.contiguous(),
+                                         img0_depth.contiguous())
         img2p, img2p_depth, back_flow02p, fw_flow02_valid = o[:, 0:3], o[:, 3:4], o[:, 4:6], o[:, 6:7]
         img2p_valid = valid * fw_flow02_valid
         img2p = img2p * img2p_valid
@@ -432,7 +436,9 @@ class PreprocessPlusAugment(nn.Module):
 
         flow13, flow13_valid = cf(back_flow01, flow01, flow03, img1_depth)             # :414
         flow13_valid = flow13_valid * img1_valid
-        o, valid, coll3p = fw(torch.cat((img1, img1_depth, flow13 * -1.0, flow13_valid), 1), flow13, img1_depth)
+        # :416-417 (fw(cat(img1, img1_depth, flow13 * -1.0, flow13_valid), flow13, img1_depth))
+        o, valid, coll3p = warp_flow_cat(torch.cat((img1, flow13_valid), 1).to(torch.float32), flow13.contiguous(),
+                                         img1_depth.contiguous())
         img3p, img3p_depth, back_flow13p, fw_flow13_valid = o[:, 0:3], o[:, 3:4], o[:, 4:6], o[:, 6:7]
         img3p_valid = valid * fw_flow13_valid
         img3p = img3p * img3p_valid

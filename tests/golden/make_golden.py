@@ -134,12 +134,29 @@ class _CpuImage(torch.Tensor):
         return "cpu"
 
 
-def load_reference_inpaint():
-    """utils.inpaint taken by AST with the recorder as cv2."""
+class _Cv2Telea(_Cv2Recorder):
+    """Stand-in cv2 whose ``inpaint`` is the oracle's restatement of OpenCV's
+    sequential Telea (oracle/inpaint_oracle.c, cv2's heap order): the uint8
+    HWC image and the fill mask cv2 would be handed go through it, and the
+    uint8 HWC result comes back, as cv2.inpaint returns it.  The mask is fed as
+    valid = (mask == 0) with no collisions, for which the oracle's mask algebra
+    (utils.py:137-142) gives back exactly this mask."""
+
+    def inpaint(self, img, mask, radius, flags):
+        assert flags == self.INPAINT_TELEA and img.dtype == np.uint8 and img.ndim == 3
+        self.calls.append((mask.sum(),))
+        planes = np.ascontiguousarray(img.transpose(2, 0, 1)[None].astype(np.float32))
+        valid = (mask == 0).astype(np.float32)[None, None]
+        out = oracle.inpaint(planes, valid, np.zeros_like(valid), int(radius), layered=False)
+        return np.ascontiguousarray(out[0].transpose(1, 2, 0).astype(np.uint8))
+
+
+def load_reference_inpaint(cv2_cls=None):
+    """utils.inpaint taken by AST with the recorder (or another stand-in) as cv2."""
     src = open(os.path.join(REF, "utils.py")).read()
     tree = ast.parse(src)
     body = [n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name == "inpaint"]
-    rec = _Cv2Recorder()
+    rec = (cv2_cls or _Cv2Recorder)()
     mod = types.ModuleType("utils_inpaint")
     mod.__dict__.update(torch=torch, np=np, cv2=rec)
     exec(compile(ast.Module(body=body, type_ignores=[]), os.path.join(REF, "utils.py"), "exec"), mod.__dict__)
@@ -464,6 +481,79 @@ def make_ppa_forward_cases(utils_mod, ref_fw, Convert):
     return cases
 
 
+# the flows of files that pass through geometry evaluated on the device: the
+# group's ego-motion flows (channels 28:44) and the rotation augmentations
+# (type 6); everything else must match bit for bit (tests/test_preprocess.py)
+FILL_TOL_GROUP_CH = tuple(range(28, 44))
+
+
+def _tol_channels(key, kind):
+    if key == "group":
+        return FILL_TOL_GROUP_CH
+    if kind != 6:
+        return ()
+    return (4, 5, 6, 7) if key.endswith("_1") else (0, 1, 2, 3)
+
+
+def make_ppa_fill_cases(utils_mod, ref_fw, Convert):
+    """PreprocessPlusAugment.forward (:329-476) of two 32x40 images with the
+    real hole-fill: the reference's text slices run with utils.inpaint backed
+    by _Cv2Telea (cv2's sequential Telea, restated by the oracle), the oracle
+    as fw_cuda.  Every file forward writes is pinned per channel: a SHA-256
+    digest of the channel (bit-exact bar), plus the float32 values of the
+    channels held to the 1e-5 px geometry tolerance, and a strided sample of
+    every channel for readable failures.  ``holes`` counts the pixels each
+    image's 95 fills actually filled (the fill is not idle)."""
+    import tempfile
+    import torch.nn as nn
+    lines = open(os.path.join(REF, "preprocess.py")).read().split("\n")
+    assert lines[462].rstrip().endswith("axis=0"), lines[462]
+    body = lines[328:476]
+    body[462 - 328] = lines[462] + ")"  # the missing parenthesis of :463
+    ns = dict(torch=torch, nn=nn, np=np, os=os, sys=sys, time=__import__("time"), math=math,
+              utils=utils_mod, FW=ref_fw.FW, Convert=Convert, device="cpu")
+    for a, b in ((301, 326), (24, 182)):
+        exec(compile("\n".join(lines[a - 1:b]), os.path.join(REF, "preprocess.py"), "exec"), ns)
+    exec(compile("\n".join(body), os.path.join(REF, "preprocess.py"), "exec"), ns)
+    h, w = 32, 40
+    cases = {"h": np.array(h), "w": np.array(w)}
+    ref_inpaint, tel = load_reference_inpaint(_Cv2Telea)
+    utils_mod.inpaint = lambda img, valid, coll: ref_inpaint(img.as_subclass(_CpuImage), valid, coll).as_subclass(
+        torch.Tensor)
+    seeds = (5150, 5151)
+    cases["seeds"] = np.array(seeds)
+    for n, seed in enumerate(seeds):
+        raw = synth_depth(h, w, seed)
+        img0 = torch.from_numpy(synth_rgb(h, w, seed))
+        cases[f"i{n}/raw_depth"] = raw
+        cases[f"i{n}/img0"] = img0.numpy()
+        ppa = ns["PreprocessPlusAugment"]("cpu")
+        tel.calls.clear()
+        with tempfile.TemporaryDirectory() as td:
+            out = os.path.join(td, "img")
+            utils_mod.set_seed(seed)
+            ppa((img0, torch.from_numpy(raw.copy()).unsqueeze(0)), out, False)
+            assert len(os.listdir(out)) == 121
+            files = {"group": (np.load(os.path.join(out, "group.npz"))["img_depth_flow"], None)}
+            for g in range(5):
+                for a in range(12):
+                    for k in (1, 2):
+                        z = np.load(os.path.join(out, f"{g}_{a}_{k}.npz"))
+                        files[f"{g}_{a}_{k}"] = (z["img_depth_flow"], int(z["augment_flow_type"]))
+        cases[f"i{n}/holes"] = np.array([c[0] for c in tel.calls], np.int64)
+        for key, (arr, kind) in files.items():
+            pre = f"i{n}/{key}"
+            cases[pre + "/dtype"] = np.array(arr.dtype.str)
+            cases[pre + "/shape"] = np.array(arr.shape)
+            if kind is not None:
+                cases[pre + "/type"] = np.array(kind)
+            cases[pre + "/digest"] = np.array([_digest(arr[c]) for c in range(arr.shape[0])])
+            cases[pre + "/sample"] = np.ascontiguousarray(arr[:, ::5, ::7]).astype(np.float32)
+            for c in _tol_channels(key, kind):
+                cases[f"{pre}/tol{c}"] = arr[c].astype(np.float32)
+    return cases
+
+
 def main():
     ref_fw = load_reference_fw()
     geometry_mod = load_reference_geometry()
@@ -474,6 +564,11 @@ def main():
         c1 = make_config1_cases(ref_fw, Convert, utils_mod)
         np.savez_compressed(os.path.join(HERE, "config1.npz"), **c1)
         print("config1.npz", os.path.getsize(os.path.join(HERE, "config1.npz")), "bytes")
+        return
+    if sys.argv[1:] == ["ppa_fill"]:  # only the forward fixture with the real (oracle-Telea) fill
+        pf = make_ppa_fill_cases(utils_mod, ref_fw, Convert)
+        np.savez_compressed(os.path.join(HERE, "ppa_fill.npz"), **pf)
+        print("ppa_fill.npz", os.path.getsize(os.path.join(HERE, "ppa_fill.npz")), "bytes")
         return
     if sys.argv[1:] == ["ppa_forward"]:  # only the per-image forward fixture
         ref_inpaint, rec = load_reference_inpaint()

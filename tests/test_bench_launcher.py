@@ -27,6 +27,12 @@ def test_bench_launches_n_ranks(n):
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == n and rec["dry_run"] is True and rec["steps"] == 3
     assert rec["shard_images"] == [0, 4]  # rank 0's contiguous shard of 4 * n images
+    # what the process group itself saw: its size, its backend, every rank's own time
+    ranks = rec["ranks"]
+    assert ranks["world_size"] == n and ranks["backend"] == "gloo"
+    assert len(ranks["ms_per_step"]) == n and all(t >= 0 for t in ranks["ms_per_step"])
+    # every rank exited cleanly after the final barrier (rank 0 sleeps before it)
+    assert "Traceback" not in r.stderr
 
 
 def test_bench_single_rank_does_not_relaunch():

@@ -124,3 +124,30 @@ def test_warp_disparity_special_depths(dtype, W, disparity_engine):
         g_ = g_.cpu().numpy()
         assert np.array_equal(g_, e_.cpu().numpy(), equal_nan=True), n
         assert np.array_equal(g_, c_, equal_nan=True), n
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("W", [8192, 8190, 8193, 8196])
+def test_disparity_row_kernel_width_limit(W):
+    """The row kernel serves rows up to kRowMaxW = 8192 (64 KB of LDS keys per
+    workgroup); wider rows fall back to the TILE engine.  Both sides of the
+    limit, with and without 16-byte vector rows (W % 4), bit-exact against the
+    TILE engine on the same call."""
+    from opticalflowfromdepth_amd import _native, warp_disparity
+    lib = _native.lib()
+    rgb, d, s, ex = _inputs(2, 3, W, torch.float32, 900 + W, extra=1)
+    dev = torch.device("cuda:0")
+    args = (torch.cat((rgb, ex), 1).to(dev), d.to(dev), s)
+    prev = lib.ofd_fw_set_disparity_rows(1)
+    try:
+        rows = warp_disparity(*args)
+        lib.ofd_fw_set_disparity_rows(0)
+        tile = warp_disparity(*args)
+    finally:
+        lib.ofd_fw_set_disparity_rows(prev)
+    for x, y in zip(rows, tile):
+        assert torch.equal(x, y)
+    obj, flow = _unfused(rgb, d, s, ex)
+    exp = oracle.fw_flow(obj.numpy(), flow.numpy(), d.to(torch.float32).numpy())
+    for g, e in zip(rows, exp):
+        assert np.array_equal(g.cpu().numpy(), e)

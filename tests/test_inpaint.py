@@ -297,6 +297,48 @@ def test_layered_vs_sequential_divergence_on_warped_images():
     assert stats["mean"] < 8.0 and stats["p99"] < 64 and stats["frac_over_32"] < 0.05, stats
 
 
+@pytest.fixture(autouse=True)
+def _no_fill_faults(request):
+    """Every GPU hole-fill test ends with no invariant-violation bit raised
+    (ofd_inpaint_faults: a layered tail wait that gave up, a sequential bucket
+    or distance sweep past its bound); each would mean an incomplete fill."""
+    yield
+    if request.node.get_closest_marker("gpu") is not None and torch.cuda.is_available():
+        from opticalflowfromdepth_amd import _native
+        torch.cuda.synchronize()
+        assert _native.lib().ofd_inpaint_faults(1) == 0
+
+
+@pytest.mark.gpu
+def test_inpaint_tail_queue_beside_a_persistent_warp():
+    """The layered fill's deep-tail kernel (schedule (0, 0): every layer on it)
+    runs while the FW warp's persistent SPLAT holds CUs on another stream: its
+    ticket queue needs no co-resident grid, so the bits stay the
+    oracle's and no wait gives up."""
+    from opticalflowfromdepth_amd import _native, forward_warp_flow, ops, synth
+    lib = _native.lib()
+    dev = torch.device("cuda:0")
+    obj, flow, depth = synth.stage_one_batch([12345, 12377], 192, 256, dev)
+    out, valid, coll = forward_warp_flow(obj, flow, depth)
+    img = (out[:, 0:3] * valid).contiguous()
+    exp = oracle.inpaint(img.cpu().numpy(), valid.cpu().numpy(), coll.cpu().numpy(), 3, layered=True)
+    big = synth.stage_one_batch([12345 + i for i in range(32)], 768, 1024, dev)
+    side = torch.cuda.Stream(dev)
+    lib.ofd_inpaint_set_schedule(0, 0)
+    try:
+        torch.cuda.synchronize()
+        for rep in range(3):
+            with torch.cuda.stream(side):
+                for _ in range(4):
+                    forward_warp_flow(*big)
+            got = ops.inpaint(img, valid, coll, order="layered")
+            torch.cuda.synchronize()
+            assert np.array_equal(got.cpu().numpy(), exp), rep
+    finally:
+        lib.ofd_inpaint_set_schedule(-1, -1)
+    assert lib.ofd_inpaint_faults(1) == 0
+
+
 @pytest.mark.gpu
 def test_inpaint_sequential_wide_image_half_unit_buckets():
     """H + W >= 8000 takes the half-unit distance buckets (the 0.7-wide ones

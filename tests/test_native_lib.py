@@ -65,6 +65,17 @@ def test_engine_switch():
     lib.ofd_fw_set_engine(cur)
 
 
+def test_row_path_switch():
+    from opticalflowfromdepth_amd import _native
+    lib = _native.lib()
+    cur = lib.ofd_fw_set_row_path(-1)
+    assert cur in (0, 1)
+    assert lib.ofd_fw_set_row_path(0) == cur
+    assert lib.ofd_fw_set_row_path(1) == 0
+    assert lib.ofd_fw_set_row_path(-1) == 1
+    lib.ofd_fw_set_row_path(cur)
+
+
 def test_disparity_rows_switch():
     from opticalflowfromdepth_amd import _native
     lib = _native.lib()
@@ -100,6 +111,9 @@ def test_inpaint_argument_errors_without_gpu():
     assert f(p, p, p, p, 1, 3, 1, 8, 3, None, 0, None) == -1          # H < 2
     assert f(p, p, p, p, 1, 3, 2048, 2049, 3, None, 0, None) == -2   # H + W > 4096
     assert f(p, p, p, p, 1, 3, 8, 8, 3, None, 0, None) == -3          # no workspace
+    g = lib.ofd_inpaint_telea_seq_f32
+    assert g(p, p, p, p, 1, 3, 2, 1 << 19, 3, None, 0, None) == -2    # H + W >= 2^19: bucket margin
+    assert g(p, p, p, p, 1, 3, 8, 8, 3, None, 0, None) == -3          # no workspace
     one = lib.ofd_inpaint_workspace_bytes(1, 768, 1024)
     assert one >= 768 * 1024 * 14
     assert lib.ofd_inpaint_workspace_bytes(4, 768, 1024) >= 4 * 768 * 1024 * 14 > one
