@@ -104,6 +104,14 @@ int ofd_fw_set_disparity_rows(int on);
  * only queries.  Returns the previous setting.  Process-wide, not thread-safe. */
 int ofd_fw_set_row_path(int on);
 
+/* PIPE variant of the TILE engine: BIN runs inside the persistent SPLAT
+ * launch (one launch per chunk instead of two; images are binned while
+ * earlier images' tiles are served, with an agent-scope release / acquire
+ * per image).  Results are identical.  on = 1 / 0 selects it for subsequent
+ * calls (also OFD_FW_PIPE=1); any other value only queries.  Returns the
+ * previous setting.  Process-wide, not thread-safe. */
+int ofd_fw_set_pipe(int on);
+
 /* Benchmark hook: when non-NULL, the given hipEvent_t's are recorded on the
  * launch stream right before the first and right after the last launch of
  * each subsequent f32 call's dominant kernel: SPLAT (TILE engine), RESOLVE

@@ -1,4 +1,4 @@
-"""Loader for the native library (libofd_fw.so; C ABI in include/ofd_fw.h and include/ofd_inpaint.h).
+"""Loader for the native library (libofd_fw.so; C ABI in include/ofd_fw.h, ofd_inpaint.h, ofd_deflate.h).
 
 The library is built in-tree by :func:`opticalflowfromdepth_amd.build.build_native`
 (hipcc --offload-arch=gfx950).  There is deliberately NO fallback: if the
@@ -34,6 +34,7 @@ SIGNATURES = {
     "ofd_fw_set_engine": ([ctypes.c_int], ctypes.c_int),
     "ofd_fw_set_disparity_rows": ([ctypes.c_int], ctypes.c_int),
     "ofd_fw_set_row_path": ([ctypes.c_int], ctypes.c_int),
+    "ofd_fw_set_pipe": ([ctypes.c_int], ctypes.c_int),
     "ofd_fw_set_profile_events": ([_P, _P], ctypes.c_int),
     "ofd_fw_workspace_bytes": ([_I64, _I64, _I64, ctypes.c_int], _SZ),
     "ofd_fw_workspace_init": ([_P, _SZ, _P], ctypes.c_int),
@@ -56,6 +57,9 @@ SIGNATURES = {
     "ofd_inpaint_telea_seq_f32": ([_P] * 4 + [_I64] * 4 + [ctypes.c_int, _P, _SZ, _P], ctypes.c_int),
     "ofd_inpaint_set_schedule": ([ctypes.c_int, ctypes.c_int], ctypes.c_int),
     "ofd_inpaint_faults": ([ctypes.c_int], ctypes.c_int),
+    "ofd_deflate_bound": ([_I64], _SZ),
+    "ofd_deflate_workspace_bytes": ([_I64, _I64], _SZ),
+    "ofd_deflate_batch": ([_P, _I64, _I64, _P, _P, _P, _P, _SZ, _P], ctypes.c_int),
 }
 
 

@@ -3,8 +3,8 @@
 ``python -m opticalflowfromdepth_amd.build`` or ``build_native()`` compiles
 csrc/ofd_fw.hip (forward warp), csrc/ofd_inpaint.hip (layered hole-fill) and
 csrc/ofd_inpaint_seq.hip (the default hole-fill, cv2's sequential Telea order)
-with hipcc into ``_build/libofd_fw.so`` (C ABI, include/ofd_fw.h and
-include/ofd_inpaint.h).
+and csrc/ofd_deflate.hip (the npz product's GPU deflate) with hipcc into
+``_build/libofd_fw.so`` (C ABI, include/ofd_fw.h, ofd_inpaint.h, ofd_deflate.h).
 The .so is git-ignored but travels with the repo snapshot to the GPU box.
 """
 from __future__ import annotations
@@ -16,8 +16,9 @@ import sys
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(_HERE)
-SRCS = [os.path.join(_HERE, "csrc", f) for f in ("ofd_fw.hip", "ofd_inpaint.hip", "ofd_inpaint_seq.hip")]
-HDRS = [os.path.join(REPO, "include", f) for f in ("ofd_fw.h", "ofd_inpaint.h")] + [
+SRCS = [os.path.join(_HERE, "csrc", f) for f in ("ofd_fw.hip", "ofd_inpaint.hip", "ofd_inpaint_seq.hip",
+                                                  "ofd_deflate.hip")]
+HDRS = [os.path.join(REPO, "include", f) for f in ("ofd_fw.h", "ofd_inpaint.h", "ofd_deflate.h")] + [
     os.path.join(_HERE, "csrc", "ip_common.h")]
 OUT_DIR = os.path.join(_HERE, "_build")
 OUT = os.path.join(OUT_DIR, "libofd_fw.so")

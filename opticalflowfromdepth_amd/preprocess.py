@@ -596,6 +596,11 @@ class NpzWriter:
 def save_group(out_dirs: Sequence[str], group44: torch.Tensor, writer: Optional[NpzWriter] = None) -> None:
     """group.npz, key img_depth_flow = [44,H,W] (preprocess.py:434-447)."""
     assert group44.shape[1] == 44, "wrong data shape"
+    if writer is not None and hasattr(writer, "save_batch"):  # GpuNpzWriter: one deflate launch for the batch
+        for d in out_dirs:
+            os.makedirs(d, exist_ok=True)
+        writer.save_batch([os.path.join(d, "group.npz") for d in out_dirs], group44.detach(), "img_depth_flow")
+        return
     for d, x in zip(out_dirs, group44.detach()):
         os.makedirs(d, exist_ok=True)
         path = os.path.join(d, "group.npz")
@@ -610,6 +615,11 @@ def save_augment(out_dirs: Sequence[str], g: int, a: int, kind: int, d1: torch.T
     """{g}_{a}_1.npz / {g}_{a}_2.npz, keys img_depth_flow [8,H,W] and
     augment_flow_type (preprocess.py:462-476)."""
     assert d1.shape[1] == 8 and d2.shape[1] == 8
+    if writer is not None and hasattr(writer, "save_batch"):
+        for k, x in ((1, d1), (2, d2)):
+            writer.save_batch([os.path.join(d, f"{g}_{a}_{k}.npz") for d in out_dirs], x.detach(), "img_depth_flow",
+                              {"augment_flow_type": np.array(kind)})
+        return
     for d, x1, x2 in zip(out_dirs, d1.detach(), d2.detach()):
         for k, x in ((1, x1), (2, x2)):
             path = os.path.join(d, f"{g}_{a}_{k}.npz")

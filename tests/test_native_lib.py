@@ -11,9 +11,9 @@ from conftest import REPO
 
 def _header_symbols():
     syms = set()
-    for h in ("ofd_fw.h", "ofd_inpaint.h"):
+    for h in ("ofd_fw.h", "ofd_inpaint.h", "ofd_deflate.h"):
         txt = open(os.path.join(REPO, "include", h)).read()
-        syms |= set(re.findall(r"\b(ofd_(?:fw|inpaint)_\w+)\s*\(", txt))
+        syms |= set(re.findall(r"\b(ofd_(?:fw|inpaint|deflate)_\w+)\s*\(", txt))
     return sorted(syms)
 
 
@@ -186,7 +186,7 @@ def test_c_abi_header_compiles_as_c():
     import tempfile
     with tempfile.TemporaryDirectory() as d:
         c = os.path.join(d, "t.c")
-        open(c, "w").write('#include "ofd_fw.h"\n#include "ofd_inpaint.h"\nint main(void){int (*f)(void) = '
+        open(c, "w").write('#include "ofd_fw.h"\n#include "ofd_inpaint.h"\n#include "ofd_deflate.h"\nint main(void){int (*f)(void) = '
                            'ofd_fw_abi_version; size_t (*g)(int64_t, int64_t, int64_t) = ofd_inpaint_workspace_bytes; '
                            '(void)f; (void)g; return OFD_FW_OK;}\n')
         subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-c", "-I", os.path.join(REPO, "include"),
