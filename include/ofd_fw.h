@@ -94,24 +94,6 @@ int ofd_fw_set_engine(int engine);
  * queries.  Returns the previous setting.  Process-wide, not thread-safe. */
 int ofd_fw_set_disparity_rows(int on);
 
-/* Row path of the TILE engine: images whose every source lands in its own row
- * (BIN checks it per image and per call; e.g. any disparity flow,
- * preprocess.py:249-254) are splatted row by row instead of through the tile
- * lists; results are identical.  Used by the float32 / float64-flow / bf16
- * flow entries and the forward_warping op when W <= 4096, W % 4 == 0 and every
- * plane is 16-byte aligned (8-byte for bf16 planes).  on = 1 / 0 enables /
- * disables it for subsequent calls (also OFD_FW_ROWPATH=0); any other value
- * only queries.  Returns the previous setting.  Process-wide, not thread-safe. */
-int ofd_fw_set_row_path(int on);
-
-/* PIPE variant of the TILE engine: BIN runs inside the persistent SPLAT
- * launch (one launch per chunk instead of two; images are binned while
- * earlier images' tiles are served, with an agent-scope release / acquire
- * per image).  Results are identical.  on = 1 / 0 selects it for subsequent
- * calls (also OFD_FW_PIPE=1); any other value only queries.  Returns the
- * previous setting.  Process-wide, not thread-safe. */
-int ofd_fw_set_pipe(int on);
-
 /* Benchmark hook: when non-NULL, the given hipEvent_t's are recorded on the
  * launch stream right before the first and right after the last launch of
  * each subsequent f32 call's dominant kernel: SPLAT (TILE engine), RESOLVE

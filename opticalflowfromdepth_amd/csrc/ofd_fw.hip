@@ -50,7 +50,6 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include <atomic>
 #include <mutex>
 #include <type_traits>
 #include <unordered_map>
@@ -183,14 +182,9 @@ __device__ __forceinline__ void load4(const T *__restrict__ q, T v[4], int n) {
     TARGET_RANGE_EXACT
 
 // Coordinate sources: the target of the source at pixel p = j*W + i of image b.
-//
-// kRowPath: the source can take the ROW path of the persistent SPLAT (row_item
-// below).  BIN checks, per image, that every source lands, and lands in its own
-// row (ty == j, as every disparity flow does: preprocess.py:249-254); such an
-// image needs only the x coordinate (load4x / target_x) to place its sources.
+
 struct SafeF32 {  // fw_cuda.forward_warping inputs: safe_y, safe_x [B,1,H,W]
     using V = float;
-    static constexpr bool kRowPath = true;
     const float *sy, *sx;
     int64_t HW;
     __device__ __forceinline__ void load(int64_t b, int64_t p, V &x, V &y) const {
@@ -202,23 +196,16 @@ struct SafeF32 {  // fw_cuda.forward_warping inputs: safe_y, safe_x [B,1,H,W]
         ::load4<kVec>(sx + b * HW + p, x, n);
         ::load4<kVec>(sy + b * HW + p, y, n);
     }
-    template <bool kVec>
-    __device__ __forceinline__ void load4x(int64_t b, int64_t p, V x[4], int n) const {
-        ::load4<kVec>(sx + b * HW + p, x, n);
-    }
     __host__ bool vec_ok() const { return (uintptr_t(sx) | uintptr_t(sy)) % 16 == 0; }
     __device__ __forceinline__ void target(int64_t, int, int, V x, V y, int H, int W, int &tx, int &ty) const {
         target_safe<float>(x, y, H, W, tx, ty);
     }
-    // target column of a source BIN has proven to land in its own row
-    __device__ __forceinline__ int target_x(int, V x, int) const { return int(x); }
     KEY_DEPTH_FROM_PLANE
 };
 
 template <typename F>
 struct FlowCoords {  // FW.forward input: flow [B,2,H,W], ch0 = x, ch1 = y
     using V = F;
-    static constexpr bool kRowPath = true;
     const F *flow;
     int64_t HW;
     __device__ __forceinline__ void load(int64_t b, int64_t p, V &x, V &y) const {
@@ -232,20 +219,9 @@ struct FlowCoords {  // FW.forward input: flow [B,2,H,W], ch0 = x, ch1 = y
         ::load4<kVec>(f, x, n);
         ::load4<kVec>(f + HW, y, n);
     }
-    template <bool kVec>
-    __device__ __forceinline__ void load4x(int64_t b, int64_t p, V x[4], int n) const {
-        ::load4<kVec>(flow + b * 2 * HW + p, x, n);
-    }
     __host__ bool vec_ok() const { return uintptr_t(flow) % 16 == 0; }
     __device__ __forceinline__ void target(int64_t, int i, int j, V x, V y, int H, int W, int &tx, int &ty) const {
         target_flow<F>(i, j, x, y, H, W, tx, ty);
-    }
-    // the x half of target_flow for a source BIN has proven to land in its own
-    // row (so p0 + flow is not NaN): the same add, clamp and truncation
-    __device__ __forceinline__ int target_x(int i, V x, int W) const {
-        F px = F(i) + x;
-        px = px < F(0) ? F(0) : (px > F(W - 1) ? F(W - 1) : px);
-        return int(px);
     }
     KEY_DEPTH_FROM_PLANE
 };
@@ -261,7 +237,6 @@ template <typename D>
 struct DisparityCoords {
     using V = D;
     static constexpr int kGen = 3, kGenGT = 8;
-    static constexpr bool kRowPath = false;  // has its own row kernel (disp_row_kernel)
     const D *depth;
     const float *s;  // [B] per-image scale
     int64_t HW;
@@ -396,7 +371,6 @@ struct EgoCoords {
     // sources has been issued, which keeps SPLAT's loads in flight together.
     using V = D;
     static constexpr int kGen = 3, kGenGT = 4;
-    static constexpr bool kRowPath = false;
     const D *depth;
     const float *P;  // [B][3][4] float32 (K @ T)[:3]
     EgoCam cam;
@@ -483,7 +457,6 @@ template <typename F, typename D>
 struct FlowCatCoords {
     using V = F;
     static constexpr int kGen = 3, kGenGT = 8;
-    static constexpr bool kRowPath = false;
     const F *flow;   // [B,2,H,W]
     const D *depth;  // [B,1,H,W]
     int64_t HW;
@@ -636,8 +609,6 @@ struct Ws {  // views of one chunk's workspace (G images)
     ushort4 *segrec;           // [G][nseg]    scratch: target tile box (t0x,t1x,t0y,t1y) of a segment
     ushort4 *blkrec;           // [G][nsb]     scratch: same per source block
     unsigned int *queue;       // [16]         persistent SPLAT: 8 per-XCD tile queues + exit count, ~0 between calls
-    unsigned int *rowflag;     // [G]          == the chunk's epoch: image not row-local (BIN), else row path
-    unsigned int *bindone;     // [G]          PIPE engine: BIN items finished per image, counting down from ~0
 };
 
 inline Ws carve(void *ws, int64_t G, int64_t HW, const TileGeom &g) {
@@ -654,8 +625,6 @@ inline Ws carve(void *ws, int64_t G, int64_t HW, const TileGeom &g) {
     w.blkrec = reinterpret_cast<ushort4 *>(p);
     p += align16(size_t(G) * g.nsb * 8);
     w.queue = reinterpret_cast<unsigned int *>(p);
-    w.rowflag = w.queue + 16;     // 64 + 8 G bytes of the 256 G bytes of per-image slack
-    w.bindone = w.rowflag + G;
     return w;
 }
 
@@ -705,13 +674,6 @@ struct ChunkArgs {  // one chunk of images
     Ws ws;
     int64_t b0;     // first image of the chunk
     int nimg;       // images in the chunk
-    // Row path (Coords::kRowPath, fused TILE engine): 0 = off; otherwise this
-    // chunk's epoch (never 0 or ~0).  BIN stores it into ws.rowflag[image] for
-    // every image with a source that does not land in its own row; SPLAT serves
-    // the other images by rows.  A flag left from an earlier call (a repeated
-    // epoch: graph replay, wrap-around) can only send a row-local image down
-    // the general tile path, which is always correct.
-    unsigned epoch;
 };
 
 // ---- BIN: wave w of workgroup blockIdx.x boxes segment blockIdx.x * kWaves + w.
@@ -734,28 +696,7 @@ __device__ __forceinline__ unsigned quad_min_pk16(unsigned v) {
 // instruction, and the segment box is a 3-step xor reduction over the quads
 // (8 readlanes and 9 single-lane stores before: 98 -> 72 us per 64 images,
 // and 76 -> 56 VGPRs, i.e. 8 waves per SIMD).
-// Stores of BIN's outputs.  kWT (the PIPE engine, whose tiles read them in
-// the same launch): write-through (sc1) stores, so the hand-off needs no
-// release fence (MI355X_MICROARCH.md, inter-workgroup visibility, R1).
-template <bool kWT>
-__device__ __forceinline__ void st_box(ushort4 *p, ushort4 v) {
-    if constexpr (kWT) {
-        const unsigned long long u = (unsigned long long)v.x | ((unsigned long long)v.y << 16) |
-                                     ((unsigned long long)v.z << 32) | ((unsigned long long)v.w << 48);
-        __hip_atomic_store(reinterpret_cast<unsigned long long *>(p), u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-        *p = v;
-    }
-}
-template <bool kWT>
-__device__ __forceinline__ void st_u32(unsigned *p, unsigned v) {
-    if constexpr (kWT)
-        __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else
-        *p = v;
-}
-
-template <typename Coords, bool kWT = false>
+template <typename Coords>
 __device__ __forceinline__ void bin_segment(const Coords &co, const float *__restrict__ depth, const ChunkArgs &a,
                                                int H, int W, int64_t HW, const TileGeom &g, int64_t sgg,
                                                const typename Coords::V (&x)[2][4], const typename Coords::V (&y)[2][4]) {
@@ -768,17 +709,13 @@ __device__ __forceinline__ void bin_segment(const Coords &co, const float *__res
     const int i0 = sgx * (SEGB * SBW) + (lane & 31) * 4;
     const int jh = sby * SBH + (lane >> 5);
     unsigned mn = 0xFFFFFFFFu, mxi = 0xFFFFFFFFu;
-    bool off_row = false;  // a source of this lane is dropped or leaves its row (row path check)
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
         const int j = jh + 2 * q;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             int tx0 = -1, tx1 = -1, ty0 = -1, ty1 = -1;
-            if (i0 + e < W && j < H) {
-                co.target_range(b, i0 + e, j, x[q][e], y[q][e], H, W, tx0, tx1, ty0, ty1);
-                if constexpr (Coords::kRowPath) off_row |= (tx0 < 0) | (ty0 != j) | (ty1 != j);
-            }
+            if (i0 + e < W && j < H) co.target_range(b, i0 + e, j, x[q][e], y[q][e], H, W, tx0, tx1, ty0, ty1);
             if (tx0 >= 0) {
                 mn = pk_min_u16(mn, unsigned(tx0 / TW) | (unsigned(ty0 / TH) << 16));
                 mxi = pk_min_u16(mxi, (0xFFFFu - unsigned(tx1 / TW)) | ((0xFFFFu - unsigned(ty1 / TH)) << 16));
@@ -802,25 +739,16 @@ __device__ __forceinline__ void bin_segment(const Coords &co, const float *__res
         smx = pk_min_u16(smx, unsigned(__shfl_xor(int(smx), m)));
     }
     if (lane < 32 && (lane & 3) == 0 && sbx < g.nsbx)
-        st_box<kWT>(ws.blkrec + int64_t(bl) * g.nsb + int64_t(sby) * g.nsbx + sbx,
-                    boxed ? make_ushort4((unsigned short)t0x, (unsigned short)t1x, (unsigned short)t0y,
-                                         (unsigned short)t1y)
-                          : empty_box());
+        ws.blkrec[int64_t(bl) * g.nsb + int64_t(sby) * g.nsbx + sbx] =
+            boxed ? make_ushort4((unsigned short)t0x, (unsigned short)t1x, (unsigned short)t0y, (unsigned short)t1y)
+                  : empty_box();
     if (lane == 0)
-        st_box<kWT>(ws.segrec + sgg,
-                    (smn & 0xFFFFu) == 0xFFFFu
-                        ? empty_box()
-                        : make_ushort4((unsigned short)(smn & 0xFFFFu), (unsigned short)(0xFFFFu - (smx & 0xFFFFu)),
-                                       (unsigned short)(smn >> 16), (unsigned short)(0xFFFFu - (smx >> 16))));
+        ws.segrec[sgg] = (smn & 0xFFFFu) == 0xFFFFu
+                             ? empty_box()
+                             : make_ushort4((unsigned short)(smn & 0xFFFFu), (unsigned short)(0xFFFFu - (smx & 0xFFFFu)),
+                                            (unsigned short)(smn >> 16), (unsigned short)(0xFFFFu - (smx >> 16)));
     // wide blocks as a bit mask over k (bit 4k of the ballot of lanes < 32)
     const unsigned long long wb = __ballot(is_wide && lane < 32 && (lane & 3) == 0);
-    // Row path: an image keeps it only if every source lands in its own row
-    // and no block spills to the key slab (the row path never merges the
-    // slab).  Every offending wave stores the same word: plain stores, no
-    // atomics; SPLAT reads it after the kernel boundary.
-    if constexpr (Coords::kRowPath) {
-        if (a.epoch != 0u && (wb != 0ull || __ballot(off_row) != 0ull) && lane == 0) st_u32<kWT>(ws.rowflag + bl, a.epoch);
-    }
     if (wb == 0ull) return;  // wave-uniform
     // non-smooth flow (rare): the wide blocks' sources go to the key slab by
     // global atomic min and flag their target tiles for SPLAT's merge
@@ -836,7 +764,7 @@ __device__ __forceinline__ void bin_segment(const Coords &co, const float *__res
             const int64_t p = int64_t(j) * W + i0 + e;
             const unsigned long long key = ok ? make_key(co.key_depth(b, p, depth), unsigned(p)) : 0ull;
             wave_run_atomic_min(ws.keys + int64_t(bl) * HW, ok ? ty * W + tx : -1, key);
-            if (ok) st_u32<kWT>(ws.flag + int64_t(bl) * g.ntiles + (ty / TH) * g.tilesX + tx / TW, 0u);
+            if (ok) ws.flag[int64_t(bl) * g.ntiles + (ty / TH) * g.tilesX + tx / TW] = 0u;
         }
 }
 
@@ -1038,9 +966,7 @@ __device__ __forceinline__ void splat_tile(TileLds &L, unsigned lin, int bl, int
     const ushort4 *blkrec = ws.blkrec + int64_t(bl) * g.nsb;
 
     if (threadIdx.x == 0) {
-        // a vector (agent-scope) load: in the PIPE engine the flag is BIN's
-        // output of this very launch, which a scalar-cache load could miss
-        L.flag = __hip_atomic_load(ws.flag + fid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        L.flag = ws.flag[fid];
         ws.flag[fid] = 0xFFFFFFFFu;  // restore the workspace invariant for the next call
         L.nseg = 0;
         L.nblk = 0;
@@ -1291,124 +1217,6 @@ __device__ __forceinline__ void splat_tile(TileLds &L, unsigned lin, int bl, int
     }
 }
 
-// ---- ROW path (persistent SPLAT, images BIN found row-local).  Every source
-// of such an image lands in its own row, so the tile machinery (segment and
-// block scans, the re-read of every source block a tile's box touches, the key
-// slab) is not needed: item `tile` of the image covers the rows
-// [tile*H/ntiles, (tile+1)*H/ntiles) -- about the rows of the tile row band
-// the index maps to -- in sub-bands of TW*TH/W rows, each folded into the LDS
-// z-buffer (the same lexmin keys) and published with 16-byte loads and stores.
-// Sources are read once (x coordinate and depth; the y coordinate is not
-// needed once BIN has shown ty == j), the winners' obj channels come from the
-// same rows.  The host enables it only with W <= TW*TH, W % 4 == 0 and every
-// plane 16-byte aligned (8-byte for bf16 planes).
-typedef float RowV4F __attribute__((ext_vector_type(4)));
-typedef unsigned short RowV4H __attribute__((ext_vector_type(4)));
-
-template <typename E>
-__device__ __forceinline__ void put4_nt(E *dst, const E v[4]) {
-    if constexpr (sizeof(E) == 4)
-        __builtin_nontemporal_store(RowV4F{v[0], v[1], v[2], v[3]}, reinterpret_cast<RowV4F *>(dst));
-    else
-        __builtin_nontemporal_store(RowV4H{v[0], v[1], v[2], v[3]}, reinterpret_cast<RowV4H *>(dst));
-}
-
-constexpr int kRowQ = 2;  // quads (4 targets) per thread in flight: fold
-constexpr int kRowQP = 2;  // ... publish (x 8 channels: 64 gathers per thread in flight, as the tile publish)
-
-template <typename Coords, typename Cfg, typename E>
-__device__ __forceinline__ void row_item(TileLds &L, int bl, int tile, const Coords &co, const float *__restrict__ depth,
-                                         const SplatIO &io, const ChunkArgs &a, int H, int W, int64_t HW,
-                                         const TileGeom &g) {
-    using V = typename Coords::V;
-    const int64_t b = a.b0 + bl;
-    const int r0 = int(int64_t(tile) * H / g.ntiles), r1 = int(int64_t(tile + 1) * H / g.ntiles);
-    const int RB = (TW * TH) / W;  // rows per sub-band (>= 1)
-    const int qpr = W >> 2;        // quads per row
-    const int C = io.C;
-    const E *ob = static_cast<const E *>(io.obj) + b * int64_t(io.Cobj) * HW;
-    E *oo = static_cast<E *>(io.out) + b * int64_t(C) * HW;
-    float *vb = io.valid + b * HW;
-    float *cb = io.coll + b * HW;
-    const unsigned uHW = unsigned(HW);
-    for (int ra = r0; ra < r1; ra += RB) {
-        const int rb = ra + RB < r1 ? ra + RB : r1;
-        const int n = (rb - ra) * W, nq = n >> 2;
-        const unsigned base = unsigned(ra) * unsigned(W);  // image-local index of the sub-band's first pixel
-        for (int k = threadIdx.x; k < n; k += Cfg::kThr) L.zk[k] = KEY_UNTOUCHED;
-        lds_barrier();
-        // fold: kRowQ quads per thread, every load issued before the first key
-        for (int q0 = threadIdx.x; q0 < nq; q0 += Cfg::kThr * kRowQ) {
-            V x[kRowQ][4];
-            float d[kRowQ][4];
-#pragma unroll
-            for (int u = 0; u < kRowQ; ++u) {
-                const int q = q0 + u * Cfg::kThr;
-                if (q < nq) {
-                    co.template load4x<true>(b, int64_t(base) + 4 * q, x[u], 4);
-                    ::load4<true>(depth + b * HW + base + 4 * q, d[u], 4);
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < kRowQ; ++u) {
-                const int q = q0 + u * Cfg::kThr;
-                if (q >= nq) break;
-                const int lr = q / qpr, i0 = (q - lr * qpr) * 4;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int tx = co.target_x(i0 + e, x[u][e], W);
-                    atomicMin(&L.zk[lr * W + tx], make_key(d[u][e], base + unsigned(4 * q + e)));
-                }
-            }
-        }
-        lds_barrier();
-        // publish: valid, collision, and the winners' C channels
-        for (int q0 = threadIdx.x; q0 < nq; q0 += Cfg::kThr * kRowQP) {
-            unsigned w[kRowQP][4];
-#pragma unroll
-            for (int u = 0; u < kRowQP; ++u) {
-                const int q = q0 + u * Cfg::kThr;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) w[u][e] = WIN_NONE;
-                if (q >= nq) break;
-                float vv[4], cv[4];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const unsigned long long key = L.zk[4 * q + e];
-                    const bool touched = key != KEY_UNTOUCHED, nowin = key == KEY_NOWIN;
-                    w[u][e] = (touched && !nowin) ? unsigned(key & 0xFFFFFFFFull) : WIN_NONE;
-                    vv[e] = touched ? 1.f : 0.f;
-                    cv[e] = nowin ? 1.f : 0.f;
-                }
-                put4_nt<float>(vb + base + 4 * q, vv);
-                put4_nt<float>(cb + base + 4 * q, cv);
-            }
-            constexpr int kCh = 8;
-            for (int c0 = 0; c0 < C; c0 += kCh) {
-                E o[kRowQP][kCh][4];
-#pragma unroll
-                for (int u = 0; u < kRowQP; ++u)
-#pragma unroll
-                    for (int cc = 0; cc < kCh; ++cc)
-#pragma unroll
-                        for (int e = 0; e < 4; ++e)
-                            o[u][cc][e] = (q0 + u * Cfg::kThr < nq && c0 + cc < C && w[u][e] != WIN_NONE)
-                                              ? ob[unsigned(c0 + cc) * uHW + w[u][e]]
-                                              : E(0);
-#pragma unroll
-                for (int u = 0; u < kRowQP; ++u) {
-                    const int q = q0 + u * Cfg::kThr;
-                    if (q >= nq) break;
-#pragma unroll
-                    for (int cc = 0; cc < kCh; ++cc)
-                        if (c0 + cc < C) put4_nt<E>(oo + unsigned(c0 + cc) * uHW + base + 4 * q, o[u][cc]);
-                }
-            }
-        }
-        if (ra + RB < r1) lds_barrier();  // the next sub-band re-initialises the z-buffer
-    }
-}
-
 using SplitCfg = SplatCfg<512, 2, 8>;  // split engine: 4 workgroups / CU, light publish
 // fused engine: 2 workgroups / CU (VGPR-bound), every target's gathers of a
 // thread (8 x C) in flight at once.  Measured at 64 x 768x1024, C = 6
@@ -1469,209 +1277,9 @@ __global__ __launch_bounds__(Cfg::kThr, Cfg::kMinW) void splat_persist_kernel(Co
         if (lin == ~0u) return;
         int bl, tile;
         tile_of<Cfg>(lin, a, g, bl, tile);
-        if constexpr (kFuse && kVec && Coords::kRowPath && !kStamp) {
-            if (a.epoch != 0u && a.ws.rowflag[bl] != a.epoch) {  // row-local image (BIN, previous launch)
-                row_item<Coords, Cfg, E>(L, bl, tile, co, depth, io, a, H, W, HW, g);
-                continue;
-            }
-        }
         splat_tile<Coords, kVec, kFuse, kStamp, Cfg, E>(L, lin, bl, tile, co, depth, io, a, H, W, HW, g, stamps);
         // splat_tile ends with LDS reads of the z-buffer; the next iteration's
         // barrier orders them before the next tile's initialisation
-    }
-}
-
-// ---- PIPE: BIN and SPLAT in ONE persistent launch.  The two-kernel TILE
-// engine pays BIN's separate pass over the flow plane, its drain and two
-// launch boundaries; here BIN items and tile items share the persistent
-// workgroups' queues, so binning image k+1 overlaps the tiles of image k.
-//
-// Work: 8 queues (queue q: the chunk's images q, q+8, ...; served first by
-// the workgroups with blockIdx % 8 == q -- one XCD under round-robin
-// placement -- so an image's records are written and read through one L2).
-// Queue q's items, for its images i_0, i_1, ...: BIN(i_0), then BIN(i_1),
-// TILES(i_0), BIN(i_2), TILES(i_1), ..., TILES(i_last): every BIN item of an
-// image precedes all of its tile items.  A BIN item is one segment run per
-// wave (kPipeSegW segments); a tile item is splat_tile / row_item.
-//
-// Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, R1): a BIN
-// item's waves store records, flags and rowflag write-through (sc1), drain
-// them and their wide-block key atomics (vmcnt), meet at a barrier, and one
-// lane counts the item in bindone[image] (counting down from ~0); no release
-// fence (one costs a write-back of the XCD's whole L2).  Before the first tile item
-// of an image, thread 0 of a workgroup polls that counter (relaxed) until all
-// of the image's BIN items are in, issues one agent-scope acquire (it drops
-// this CU's L1) and remembers the image; the workgroup's barrier then orders
-// every wave's record loads after it.  Deadlock-free with any residency:
-// items are handed out in queue order, so every BIN item a tile waits for was
-// taken earlier by a running workgroup, and BIN items never wait.  The last
-// workgroup out restores the queue words and the counters (~0) for the next
-// launch.  Results are the two-kernel engine's, bit for bit: the same BIN
-// records and flags, the same splat_tile / row_item.
-constexpr int kPipeSegW = 1;   // segments per wave of a BIN item
-constexpr int kPipeMaxImg = 128;  // images per chunk (the acquired-image mask; 10 bits in the item word)
-
-struct PipeArgs {
-    unsigned nb;   // BIN items per image
-    unsigned nt;   // tile items per image (g.ntiles)
-};
-
-// images of queue q among nimg (images q, q+8, ...)
-__device__ __forceinline__ unsigned pipe_nq(unsigned q, int nimg) {
-    return int(q) < nimg ? unsigned(nimg - 1 - int(q)) / 8u + 1u : 0u;
-}
-
-// item x of queue q -> (BIN?, chunk image, sub-index)
-__device__ __forceinline__ void pipe_item(unsigned q, unsigned x, unsigned nq, const PipeArgs &pa, bool &bin, int &bl,
-                                          unsigned &sub) {
-    unsigned k;
-    if (x < pa.nb) {
-        bin = true;
-        k = 0;
-        sub = x;
-    } else {
-        const unsigned y = x - pa.nb, blk = pa.nb + pa.nt;
-        k = y / blk;
-        const unsigned r = y - k * blk;
-        if (k + 1u >= nq) {  // the last image's block: its tiles only
-            bin = false;
-            sub = r;
-        } else if (r < pa.nb) {
-            bin = true;
-            sub = r;
-            k += 1u;
-        } else {
-            bin = false;
-            sub = r - pa.nb;
-        }
-    }
-    bl = int(q + 8u * k);
-}
-
-// thread 0: the next item as (queue << 28 | index) ... ~0u when every queue is
-// drained; the last workgroup out restores the queue words and the counters
-__device__ __forceinline__ unsigned pipe_dequeue(unsigned *queue, unsigned *bindone, unsigned home, int nimg,
-                                                 const PipeArgs &pa, unsigned &drained, unsigned &qsel) {
-    const unsigned per_img = pa.nb + pa.nt;
-    for (unsigned k = 0; k < 8u; ++k) {
-        const unsigned qx = (home + k) & 7u;
-        if ((drained >> qx) & 1u) continue;
-        const unsigned idx = ~atomicSub(queue + qx, 1u);
-        if (idx < pipe_nq(qx, nimg) * per_img) {
-            qsel = qx;
-            return idx;
-        }
-        drained |= 1u << qx;
-    }
-    if (~atomicSub(queue + 8, 1u) == gridDim.x - 1u) {
-        // every other workgroup has finished: restore queues and counters
-        for (int k = 0; k < 9; ++k) atomicExch(queue + k, ~0u);
-        for (int b = 0; b < nimg; ++b) atomicExch(bindone + b, ~0u);
-    }
-    return ~0u;
-}
-
-// One BIN item: wave w of the workgroup bins segments (sub * kWaves + w) *
-// kPipeSegW + s of image bl, loads of all its segments in flight first.
-template <typename Coords, bool kVec>
-__device__ __forceinline__ void pipe_bin_item(const Coords &co, const float *__restrict__ depth, const ChunkArgs &a,
-                                              int bl, unsigned sub, int H, int W, int64_t HW, const TileGeom &g) {
-    using V = typename Coords::V;
-    const int lane = lane_id(), wave = threadIdx.x >> 6;
-    const int s0 = (int(sub) * kWaves + wave) * kPipeSegW;
-    V x[kPipeSegW][2][4], y[kPipeSegW][2][4];
-#pragma unroll
-    for (int s = 0; s < kPipeSegW; ++s) {
-        const int sg = s0 + s < g.nseg ? s0 + s : g.nseg - 1;  // a clamped duplicate is loaded, not binned
-        const int sby = sg / g.nsegx, sgx = sg - sby * g.nsegx;
-        const int i0 = sgx * (SEGB * SBW) + (lane & 31) * 4;
-        const int jh = sby * SBH + (lane >> 5);
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const int j = jh + 2 * q;
-            if (i0 < W && j < H) co.template load4<kVec>(a.b0 + bl, int64_t(j) * W + i0, x[s][q], y[s][q], W - i0);
-        }
-    }
-#pragma unroll
-    for (int s = 0; s < kPipeSegW; ++s)
-        if (s0 + s < g.nseg)
-            bin_segment<Coords, true>(co, depth, a, H, W, HW, g, int64_t(bl) * g.nseg + s0 + s, x[s], y[s]);
-}
-
-template <typename Coords, bool kVec, typename Cfg = FusedCfg, typename E = float>
-__global__ __launch_bounds__(Cfg::kThr, Cfg::kMinW) void splat_pipe_kernel(Coords co, const float *__restrict__ depth,
-                                                                     SplatIO io, ChunkArgs a, PipeArgs pa, int H,
-                                                                     int W, int64_t HW, TileGeom g) {
-    __shared__ TileLds L;
-    // thread 0's state, kept in LDS (registers are the tile path's)
-    __shared__ unsigned long long s_acq[kPipeMaxImg / 64];  // images whose BIN it has acquired
-    __shared__ unsigned s_drained;                          // queues seen empty
-    unsigned *queue = a.ws.queue;
-    const unsigned home = blockIdx.x % 8u;
-    if (threadIdx.x == 0) {
-        s_drained = 0u;
-        for (int k = 0; k < kPipeMaxImg / 64; ++k) s_acq[k] = 0ull;
-    }
-    for (;;) {
-        if (threadIdx.x == 0) {
-            unsigned q = 0, drained = s_drained;
-            const unsigned x = pipe_dequeue(queue, a.ws.bindone, home, a.nimg, pa, drained, q);
-            s_drained = drained;
-            unsigned long long *acq = s_acq;
-            unsigned packed = ~0u;
-            if (x != ~0u) {
-                bool bin;
-                int bl;
-                unsigned sub;
-                pipe_item(q, x, pipe_nq(q, a.nimg), pa, bin, bl, sub);
-                if (!bin && !((acq[bl >> 6] >> (bl & 63)) & 1ull)) {
-                    // every BIN item of the image was handed out before this
-                    // tile: wait for them, then drop this CU's stale L1 lines
-                    const unsigned want = ~0u - pa.nb;
-                    for (unsigned spin = 0;
-                         __hip_atomic_load(a.ws.bindone + bl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want;
-                         ++spin) {
-                        __builtin_amdgcn_s_sleep(1);
-                        if (spin == (1u << 26)) break;  // unreachable (see above); bounded all the same
-                    }
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    acq[bl >> 6] |= 1ull << (bl & 63);
-                }
-                // the image's row-path verdict, read here by one vector load
-                // (never the scalar cache: BIN wrote it in this launch)
-                const bool rows = !bin && a.epoch != 0u &&
-                                  __hip_atomic_load(a.ws.rowflag + bl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
-                                      a.epoch;
-                packed = (bin ? 0x80000000u : 0u) | (rows ? 0x40000000u : 0u) | (unsigned(bl) << 20) | sub;
-            }
-            L.next = packed;
-        }
-        lds_barrier();
-        const unsigned packed = L.next;
-        if (packed == ~0u) return;
-        const int bl = int((packed >> 20) & 0x3FFu);
-        const unsigned sub = packed & 0xFFFFFu;
-        if (packed & 0x80000000u) {
-            pipe_bin_item<Coords, kVec>(co, depth, a, bl, sub, H, W, HW, g);
-            // publish (R1): every wave's write-through stores and atomics
-            // drained, the workgroup's barrier, then one lane counts the item
-            // -- no release fence (it would write back the whole L2, with the
-            // tiles' output in it)
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            lds_barrier();
-            if (threadIdx.x == 0)
-                __hip_atomic_fetch_sub(a.ws.bindone + bl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            continue;
-        }
-        const int tile = int(sub);
-        if constexpr (Coords::kRowPath && kVec) {
-            if (packed & 0x40000000u) {  // row-local image (its BIN items, acquired above)
-                row_item<Coords, Cfg, E>(L, bl, tile, co, depth, io, a, H, W, HW, g);
-                continue;
-            }
-        }
-        splat_tile<Coords, kVec, true, false, Cfg, E>(L, 0u, bl, tile, co, depth, io, a, H, W, HW, g, nullptr);
     }
 }
 
@@ -1923,46 +1531,6 @@ unsigned persist_grid(unsigned tiles) {
     return tiles < slots ? tiles : slots;
 }
 
-// Row path of the persistent SPLAT (row_item): on by default; OFD_FW_ROWPATH=0
-// or ofd_fw_set_row_path(0) turns it off (A/B and tests).
-int g_row_path = -1;
-
-bool row_path_enabled() {
-    static const bool env_on = [] {
-        const char *e = getenv("OFD_FW_ROWPATH");
-        return !(e && e[0] == '0');
-    }();
-    return g_row_path < 0 ? env_on : g_row_path != 0;
-}
-
-// A fresh chunk epoch for the row path: never 0 (off) or ~0 (the value an
-// initialised workspace holds).
-std::atomic<unsigned> g_epoch{0};
-unsigned next_epoch() {
-    for (;;) {
-        const unsigned e = g_epoch.fetch_add(1u, std::memory_order_relaxed) + 1u;
-        if (e != 0u && e != ~0u) return e;
-    }
-}
-
-template <typename Coords, bool kVec, typename Cfg, typename E>
-unsigned pipe_grid(unsigned items) {
-    static const unsigned slots = resident_slots(splat_pipe_kernel<Coords, kVec, Cfg, E>, Cfg::kThr);
-    return items < slots ? items : slots;
-}
-
-// PIPE engine (splat_pipe_kernel): off by default until measured;
-// OFD_FW_PIPE=1 or ofd_fw_set_pipe(1) turns it on.
-int g_pipe = -1;
-
-bool pipe_enabled() {
-    static const bool env_on = [] {
-        const char *e = getenv("OFD_FW_PIPE");
-        return e && e[0] == '1';
-    }();
-    return g_pipe < 0 ? env_on : g_pipe != 0;
-}
-
 // Optional timing hook (ofd_fw_set_profile_events): events recorded on the
 // launch stream right before the first and right after the last RESOLVE
 // launch of a call -- the dominant kernel -- so a benchmark can time it with
@@ -1996,11 +1564,7 @@ int run_f32(Coords co, const E *obj, const float *depth, E *out, float *valid, f
     // measured best (a two-stream pipeline of small, cache-resident chunks
     // lost: ~10 us per cross-stream event hop, and the latency-bound BIN ran
     // 3-4x slower beside a streaming RESOLVE).
-    // PIPE engine (BIN inside the persistent SPLAT): chunks of at most
-    // kPipeMaxImg images
-    const bool pipe = mode == Mode::Tile && pipe_enabled();
-    int64_t G = chunk_images(B, HW, per_image, ws_bytes);
-    if (pipe && G > kPipeMaxImg) G = kPipeMaxImg;
+    const int64_t G = chunk_images(B, HW, per_image, ws_bytes);
     if (G < 1) return OFD_FW_EWORKSPACE;
     const int64_t nch = (B + G - 1) / G;
     if (claim_layout(ws, LayoutSig{H, W, G, 1})) {
@@ -2010,14 +1574,10 @@ int run_f32(Coords co, const E *obj, const float *depth, E *out, float *valid, f
     const Ws slab = carve(ws, G, HW, g);
     // 16-byte coordinate / depth loads in BIN and SPLAT
     const bool vec = W % 4 == 0 && co.vec_ok() && uintptr_t(depth) % 16 == 0;
-    // row path: 16-byte (8-byte for bf16) output, valid and collision stores
-    const bool row_path = Coords::kRowPath && mode == Mode::Tile && vec && W <= TW * TH && row_path_enabled() &&
-                          aligned(out, 4 * sizeof(E)) && aligned(valid, 16) && aligned(coll, 16);
     for (int64_t c = 0; c < nch; ++c) {
         const int64_t b0 = c * G;
         const int64_t nb = (B - b0) < G ? (B - b0) : G;
         const int64_t px = nb * HW;
-        const unsigned epoch = row_path ? next_epoch() : 0u;
         if constexpr (!kTileOnly) {
             if (mode == Mode::Atomic) {
                 hipLaunchKernelGGL((splat_atomic_kernel<Coords>), dim3(grid_for(px, kBlock * 4)), dim3(kBlock), 0,
@@ -2030,25 +1590,8 @@ int run_f32(Coords co, const E *obj, const float *depth, E *out, float *valid, f
             }
         }
         {
-            const ChunkArgs a{slab, b0, int(nb), epoch};
+            const ChunkArgs a{slab, b0, int(nb)};
             const SplatIO io{valid, coll, obj, out, int(C), int(C) - Coords::kGen, gen_at};
-            if (pipe) {
-                using Cfg = FusedCfgFor<Coords>;
-                const PipeArgs pa{unsigned((g.nseg + kWaves * kPipeSegW - 1) / (kWaves * kPipeSegW)),
-                                  unsigned(g.ntiles)};
-                const unsigned items = unsigned(nb) * (pa.nb + pa.nt);
-                if (c == 0 && g_prof_start) (void)hipEventRecord(g_prof_start, st);
-                if (vec)
-                    hipLaunchKernelGGL((splat_pipe_kernel<Coords, true, Cfg, E>),
-                                       dim3(pipe_grid<Coords, true, Cfg, E>(items)), dim3(Cfg::kThr), 0, st, co,
-                                       depth, io, a, pa, int(H), int(W), HW, g);
-                else
-                    hipLaunchKernelGGL((splat_pipe_kernel<Coords, false, Cfg, E>),
-                                       dim3(pipe_grid<Coords, false, Cfg, E>(items)), dim3(Cfg::kThr), 0, st, co,
-                                       depth, io, a, pa, int(H), int(W), HW, g);
-                if (c == nch - 1 && g_prof_stop) (void)hipEventRecord(g_prof_stop, st);
-                continue;
-            }
             const dim3 bgrid(grid_for(nb * g.nseg, kWaves * kBinSPW));
             if (vec)
                 hipLaunchKernelGGL((bin_kernel<Coords, true, kBinSPW>), bgrid, dim3(kWarpThreads), 0, st, co, depth, a,
@@ -2230,18 +1773,6 @@ int ofd_fw_set_profile_events(void *start_event, void *stop_event) {
 int ofd_fw_set_disparity_rows(int on) {
     const int prev = disp_row_enabled() ? 1 : 0;
     if (on == 0 || on == 1) g_disp_rows = on;
-    return prev;
-}
-
-int ofd_fw_set_pipe(int on) {
-    const int prev = pipe_enabled() ? 1 : 0;
-    if (on == 0 || on == 1) g_pipe = on;
-    return prev;
-}
-
-int ofd_fw_set_row_path(int on) {
-    const int prev = row_path_enabled() ? 1 : 0;
-    if (on == 0 || on == 1) g_row_path = on;
     return prev;
 }
 

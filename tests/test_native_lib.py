@@ -65,17 +65,6 @@ def test_engine_switch():
     lib.ofd_fw_set_engine(cur)
 
 
-def test_row_path_switch():
-    from opticalflowfromdepth_amd import _native
-    lib = _native.lib()
-    cur = lib.ofd_fw_set_row_path(-1)
-    assert cur in (0, 1)
-    assert lib.ofd_fw_set_row_path(0) == cur
-    assert lib.ofd_fw_set_row_path(1) == 0
-    assert lib.ofd_fw_set_row_path(-1) == 1
-    lib.ofd_fw_set_row_path(cur)
-
-
 def test_disparity_rows_switch():
     from opticalflowfromdepth_amd import _native
     lib = _native.lib()

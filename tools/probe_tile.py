@@ -65,7 +65,8 @@ def main():
     lib.probe_slab_bytes.restype = ctypes.c_size_t
     dev = torch.device("cuda:0")
     B, H, W = int(os.environ.get("B", "64")), 768, 1024
-    obj, flow, depth = synth.stage_one_batch([12345 + i for i in range(B)], H, W, dev)
+    obj, flow, depth = synth.stage_one_batch([12345 + i for i in range(B)], H, W, dev,
+                                             ego_fraction=float(os.environ.get("EGO", "0.5")))
     C = obj.shape[1]
     out, valid, coll = torch.empty_like(obj), torch.empty_like(depth), torch.empty_like(depth)
     slab = torch.full((lib.probe_slab_bytes(B, H, W),), 255, dtype=torch.uint8, device=dev)
