@@ -6,7 +6,8 @@ writing the 121 npz files per image.
 usage: python tools/pipeline_time.py [B H W] [--save MODE ...] [--dir D]
   MODE: none (compute only), sync (np.savez_compressed in the caller, the
   reference's way, preprocess.py:446/:471), poolN:L (NpzWriter with N threads
-  at zlib level L; 6 = numpy's level).
+  at zlib level L; 6 = numpy's level), gpuN (GpuNpzWriter: arrays deflated on
+  the GPU, N host threads assemble and write the zips).
 """
 import argparse
 import os
@@ -43,6 +44,9 @@ for mode in args.save:
         n, level = mode[4:].split(":")
         workers, level = int(n), int(level)
     ppa = pp.PreprocessPlusAugment(dev, writer_workers=workers, compresslevel=level)
+    if mode.startswith("gpu"):
+        from opticalflowfromdepth_amd.npz_gpu import GpuNpzWriter
+        ppa.writer = GpuNpzWriter(workers=int(mode[3:] or 8))
     out = None
     if mode != "none":
         base = tempfile.mkdtemp(prefix="ppa_", dir=root)
