@@ -492,6 +492,15 @@ def dry_run(args, world, rank):
     finish(world)
 
 
+_T0 = time.perf_counter()
+
+
+def progress(msg: str) -> None:
+    """One line per phase on stderr (stdout carries only the JSON line), so a
+    watchdog on silent output never mistakes the later phases for a hang."""
+    print(f"# bench {time.perf_counter() - _T0:7.1f}s: {msg}", file=sys.stderr, flush=True)
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse(argv)
@@ -531,6 +540,7 @@ def main(argv=None):
     _native.lib().ofd_fw_set_engine({"tile": 0, "atomic": 1, "split": 2}[args.engine])
     torch.cuda.synchronize()
 
+    progress(f"inputs ready ({B}x{C}x{H}x{W}); warmup")
     for _ in range(args.warmup):
         forward_warp_flow(obj, flow, depth, out=out)
     torch.cuda.synchronize()
@@ -616,26 +626,33 @@ def main(argv=None):
     cpu = None
     threads = args.cpu_threads if args.cpu_threads > 0 else min(16, os.cpu_count() or 1)
     cpu_on = rank == 0 and world == 1 and not args.no_cpu_baseline
+    progress(f"headline {wall / args.steps * 1e3:.4f} ms/step")
     if cpu_on:
+        progress("cpu baseline")
         cpu = cpu_baseline(obj, flow, depth, args.cpu_seconds, threads)
 
     cfg2 = None
     if rank == 0 and not args.no_config2:
+        progress("config 2")
         cfg2 = config2_phase(20, dev, stream, threads, args.cpu_seconds / 2 if cpu_on else 0)
 
     fused = fused_ego = None
     if rank == 0 and not args.no_fused:
+        progress("fused warps")
         fused = fused_disparity_phase(B, H, W, 10, dev, stream)
         fused_ego = fused_ego_phase(B, H, W, 10, dev, stream)
 
     bf16 = None
     if rank == 0 and not args.no_bf16:
+        progress("bf16 warp")
         bf16 = bf16_warp_phase(64, 368, 560, 20, dev, stream)
 
     hole = None
     if rank == 0 and not args.no_hole_fill:  # untimed by the driver's clock contract: after the K steps
+        progress("hole-fill")
         rgb, res, hole = hole_fill_phase(out[0], out[1], out[2], args.hole_fill_steps, stream)
         if cpu_on:
+            progress("hole-fill cpu baseline")
             (hole["cpu_baseline"], hole["layered"]["divergence_vs_sequential"],
              hole["sequential_vs_oracle"]) = hole_fill_cpu_baseline(rgb, out[1], out[2], res, args.cpu_seconds,
                                                                     threads)

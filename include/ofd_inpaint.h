@@ -33,8 +33,8 @@
  *       call); caller-owned scratch, no initialisation needed.
  *   ofd_inpaint_set_schedule
  *       no reference counterpart: diagnostics / tests only (how many hole
- *       layers are launched one by one before the persistent deep-tail kernel
- *       takes over, and the layer size below which every hole takes the
+ *       layers are launched one by one before the one-workgroup deep-tail
+ *       kernel takes over, and the layer size below which every hole takes the
  *       wave-per-hole path).  Results never depend on it.
  *
  * The call never blocks the host: every launch reads its layer's size from
@@ -89,15 +89,15 @@ int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float 
                               size_t workspace_bytes, void *stream);
 
 /* Diagnostics: launch_layers >= 0 launches exactly that many hole layers one
- * by one (the deep-tail kernel does the rest); thin_cap >= 0 sets the layer
+ * by one (the one-workgroup deep-tail kernel does the rest); thin_cap >= 0 sets the layer
  * size up to which every hole takes the wave path.  -1 restores the
  * defaults (launches sized from an earlier call's depth; thin_cap 4096).
  * Process-wide; returns 0. */
 int ofd_inpaint_set_schedule(int launch_layers, int thin_cap);
 
 /* Test / debug hook: the OR of the invariant-violation bits any hole-fill
- * kernel raised since the last reset -- 1: a layered tail-kernel wait gave up;
- * 2: a sequential-march bucket index passed its bound; 4: a sequential
+ * kernel raised since the last reset (the layered fill waits on nothing and
+ * raises none) -- 2: a sequential-march bucket index passed its bound; 4: a sequential
  * distance sweep passed its iteration bound.  Each is unreachable while the
  * algorithm's invariants hold, and each means that call's output is
  * incomplete.  Blocking (a device-to-host copy of the fault words); reset != 0

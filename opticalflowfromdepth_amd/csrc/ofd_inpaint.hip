@@ -30,8 +30,8 @@
 //          histograms, one scan, one scatter); the counts stay on the device.
 //   LAYERS one launch per outer-band layer and per hole layer over every
 //          image of the chunk, each reading its layer's size and offset from
-//          the device; a persistent tail kernel (grid barrier between layers)
-//          runs any layer deeper than the launches.  Grids and the number of
+//          the device; a one-workgroup tail kernel runs any layer deeper
+//          than the launches (no inter-workgroup waits anywhere).  Grids and the number of
 //          launches come from recent calls' counts read back asynchronously
 //          (LaggedStats): the host never waits.
 //
@@ -56,8 +56,9 @@
 
 #pragma clang fp contract(off)
 
-// Fault word of the layered fill (ofd_inpaint_faults): bit 0 = a tail-kernel
-// wait gave up (should be unreachable, see below).
+// Fault word of the layered fill (ofd_inpaint_faults): no layered kernel
+// waits on another workgroup, so it has no bit of its own (bits 1-2 are the
+// sequential fill's).
 __device__ unsigned g_ip_fault;
 
 unsigned ofd_sq_fault_read(int reset);  // ofd_inpaint_seq.hip
@@ -733,8 +734,6 @@ __global__ __launch_bounds__(1024) void ip_scan_kernel(const unsigned *__restric
     }
     if (tid == 0) {
         meta[0] = lmax;
-        meta[1] = 0u;  // the deep tail kernel's ticket counter
-        meta[2] = 0u;  // ... and its finished-block counter
     }
 }
 
@@ -1145,7 +1144,7 @@ __device__ __forceinline__ void hole_wave_lds(const Chunk &ch, const uint32_t *_
 // rest of the grid the others (wave per hole), each part grid-stride.  The
 // two sets of a layer are independent; every block runs one path.
 // Block `bx` of a G-block partition of hole layer L (a launch's blockIdx.x /
-// gridDim.x, or the tail kernel's ticket).
+// gridDim.x, or one of the tail kernel's kTailParts parts).
 __device__ __forceinline__ void hole_layer_body(const Chunk &ch, const uint32_t *__restrict__ list,
                                                 const unsigned *__restrict__ hist, const unsigned *__restrict__ cursor,
                                                 int nring, unsigned L, int range, unsigned thin_cap, WavePatch *patch,
@@ -1200,66 +1199,29 @@ __global__ __launch_bounds__(256) void ip_hole_layer_kernel(Chunk ch, const uint
 }
 
 // The layers beyond the ones the host launched (L0 .. meta[0], the deepest
-// layer the sort found), as a ticket queue that needs NO co-residency:
-// ticket t is block t % G of layer L0 + t / G (the partition a G-block layer
-// launch would use).  A workgroup takes a ticket (meta[1]), waits until every
-// block of the earlier tail layers has finished (meta[2] >= (t / G) * G),
-// runs its block, releases its stores and counts it done.  Tickets are handed
-// out in order, so every block a ticket waits for was taken earlier by a
-// workgroup that is running and waits only on still earlier tickets: the queue
-// drains whatever number of workgroups is resident (other streams' kernels may
-// hold CUs).  Exits at once when meta[0] < L0 (the usual case: the host sizes
-// its launches from the previous calls' depth).  meta[1], meta[2] are zeroed
-// by ip_scan_kernel before every call's tail.
+// layer the sort found), in ONE workgroup: layer after layer, each as the
+// kTailParts blocks of a kTailParts-block launch run one after another, a
+// workgroup barrier between layers (one CU: the layer's T / colour stores are
+// visible to every wave of the workgroup after it).  Nothing waits on another
+// workgroup, so no co-residency is assumed (other streams' kernels may hold
+// the CUs).  Exits at once when meta[0] < L0: the host launches every layer
+// of the recent calls at this shape (and every possible one when it has no
+// statistics yet), so the tail only sees a call deeper than those.
+constexpr unsigned kTailParts = 16;
 __global__ __launch_bounds__(256) void ip_hole_tail_kernel(Chunk ch, const uint32_t *__restrict__ list,
                                                            const unsigned *__restrict__ hist,
-                                                           const unsigned *__restrict__ cursor, unsigned *meta,
+                                                           const unsigned *__restrict__ cursor, const unsigned *meta,
                                                            int nring, unsigned L0, int range, unsigned thin_cap) {
     __shared__ WavePatch patch[4];
-    __shared__ unsigned s_ticket;
     const unsigned lmax = meta[0];
-    if (lmax < L0) return;
-    const unsigned G = gridDim.x, total = (lmax - L0 + 1u) * G;
-    for (;;) {
-        if (threadIdx.x == 0) {
-            const unsigned t = __hip_atomic_fetch_add(meta + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (t < total) {
-                const unsigned need = (t / G) * G;
-                // bounded (~seconds): the wait is on running workgroups only,
-                // so it ends; a give-up is recorded, never silent
-                unsigned spin = 0;
-                while (__hip_atomic_load(meta + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
-                    __builtin_amdgcn_s_sleep(2);
-                    if (++spin == (1u << 28)) {
-                        atomicOr(&g_ip_fault, 1u);
-                        break;
-                    }
-                }
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-            s_ticket = t;
-        }
+    for (unsigned L = L0; L <= lmax; ++L) {
+        for (unsigned bx = 0; bx < kTailParts; ++bx)
+            hole_layer_body(ch, list, hist, cursor, nring, L, range, thin_cap, patch, bx, kTailParts);
         __syncthreads();
-        const unsigned t = s_ticket;
-        if (t >= total) return;
-        hole_layer_body(ch, list, hist, cursor, nring, L0 + t / G, range, thin_cap, patch, t % G, G);
-        // publish the block: every wave's stores drained, then one release + count
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_fetch_add(meta + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
     }
 }
 
 inline unsigned blocks_for(unsigned n, unsigned per) { return (n + per - 1) / per; }
-
-// Layers launched one by one before the deep tail kernel takes over, when no
-// earlier call at this shape has reported its depth yet.
-constexpr int kDefaultLayers = 64;
 
 // Layers of at most this many holes run every hole on the wave path
 // (OFD_IP_THIN or ofd_inpaint_set_schedule override; probes and tests).
@@ -1286,19 +1248,6 @@ unsigned default_layer_grid() {
     return v;
 }
 
-// The deep tail kernel's grid: one 256-thread workgroup per CU (its tickets
-// do not need them resident together).
-unsigned tail_grid() {
-    static const unsigned v = [] {
-        int dev = 0, cus = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                                    hipSuccess || cus <= 0)
-            cus = 256;
-        return unsigned(cus);
-    }();
-    return v;
-}
-
 // Per-shape layer statistics of recent calls, read back without ever
 // blocking the host: every call enqueues an asynchronous copy of its layer
 // histogram and depth into pinned memory behind an event; a later call uses
@@ -1308,7 +1257,7 @@ unsigned tail_grid() {
 // caller that alternates shallow and deep fills at one shape (the pipeline's
 // flip / rotation / shear augmentations) then launches the deep calls' layers
 // -- an unneeded layer launch costs ~1.6 us, a layer left to the one-
-// workgroup-per-CU tail kernel several times a launched layer.
+// workgroup tail kernel runs on a single CU.
 struct LaggedStats {
     static constexpr size_t kHistory = 8;
     std::mutex mu;
@@ -1391,7 +1340,7 @@ int ofd_inpaint_faults(int reset) {
     }
     const unsigned q = ofd_sq_fault_read(reset);
     if (q == ~0u) return -1;
-    return int((v & 1u) | (q & 6u));
+    return int(v | (q & 6u));
 }
 
 int ofd_inpaint_set_schedule(int launch_layers, int thin_cap) {
@@ -1479,8 +1428,10 @@ int ofd_inpaint_telea_f32(const float *img, const float *valid, const float *col
                                hist, cursor, unsigned(L));
         hipLaunchKernelGGL(ip_negate_kernel, dim3(lag.valid ? std::max(16u, std::min(gdef, lag.ring / 256u + 4u)) : gdef),
                            dim3(256), 0, st, w.T, w.list, cursor, nring);
+        // no statistics yet at this shape: every possible layer (an empty
+        // launch costs ~1.6 us), so the one-workgroup tail is left idle
         const int lmax_launch = g_launch_layers >= 0 ? std::min(g_launch_layers, int(H + W))
-                                : int(lag.valid ? std::min<unsigned>(lag.lmax + 2u, unsigned(H + W)) : kDefaultLayers);
+                                : int(lag.valid ? std::min<unsigned>(lag.lmax + 2u, unsigned(H + W)) : unsigned(H + W));
         for (int L = 1; L <= lmax_launch; ++L) {
             const int bi = nring + 2 * (L - 1);
             unsigned g = gdef;
@@ -1494,7 +1445,7 @@ int ofd_inpaint_telea_f32(const float *img, const float *valid, const float *col
             hipLaunchKernelGGL(ip_hole_layer_kernel, dim3(g), dim3(256), 0, st, ch, w.list, hist, cursor, nring,
                                unsigned(L), r, thin_cap);
         }
-        hipLaunchKernelGGL(ip_hole_tail_kernel, dim3(tail_grid()), dim3(256), 0, st, ch, w.list, hist, cursor, meta,
+        hipLaunchKernelGGL(ip_hole_tail_kernel, dim3(1), dim3(256), 0, st, ch, w.list, hist, cursor, meta,
                            nring, unsigned(lmax_launch + 1), r, thin_cap);
         lagged_stats(nb, H, W, r).record(hist, meta, nbins, st);
     }

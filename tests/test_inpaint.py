@@ -223,6 +223,34 @@ def test_inpaint_sequential_after_warp_headline_shape():
 
 
 @pytest.mark.gpu
+def test_inpaint_layered_deep_ego_layers_every_schedule():
+    """The bench's own images (shard seeds: ego-motion border bands ~300 hole
+    layers deep at 768x1024) through the layered fill: the first call at a
+    shape (no statistics: every possible layer launched), the one-workgroup
+    tail taking every layer past 64, and a call sized from the statistics --
+    all the layered oracle's bits, no fault bit."""
+    from opticalflowfromdepth_amd import _native, forward_warp_flow, ops, shard, synth
+    lib = _native.lib()
+    dev = torch.device("cuda:0")
+    seeds = [shard.image_seed(i) for i in range(3)]
+    obj, flow, depth = synth.stage_one_batch(seeds, 768, 1024, dev, ego_fraction=0.67)
+    out, valid, coll = forward_warp_flow(obj, flow, depth)
+    rgb = (out[:, 0:3] * valid).contiguous()
+    exp = oracle.inpaint(rgb.cpu().numpy(), valid.cpu().numpy(), coll.cpu().numpy(), 3, layered=True)
+    lib.ofd_inpaint_faults(1)
+    try:
+        for sched in ((-1, -1), (64, -1), (-1, -1)):
+            lib.ofd_inpaint_set_schedule(*sched)
+            got = ops.inpaint(rgb, valid, coll, order="layered")
+            torch.cuda.synchronize()
+            bad = np.argwhere(got.cpu().numpy() != exp)
+            assert bad.size == 0, f"{sched}: {len(bad)} differing, first {bad[:5].tolist()}"
+    finally:
+        lib.ofd_inpaint_set_schedule(-1, -1)
+    assert lib.ofd_inpaint_faults(1) == 0
+
+
+@pytest.mark.gpu
 def test_inpaint_reference_call_shape_and_device():
     """utils.inpaint(img[3,H,W], valid[1,H,W], collision[1,H,W]) -> float32 [3,H,W] on img's device."""
     from opticalflowfromdepth_amd import utils
@@ -253,7 +281,7 @@ def test_inpaint_after_warp_headline_shape():
                          ids=["tail-only-thread", "tail-only-wave", "1-launch", "3-launches-thin64", "default"])
 def test_inpaint_gpu_schedules_bit_exact(sched):
     """Every schedule of the hole layers -- one launch per layer or the
-    persistent deep-tail kernel with grid barriers, thread or wave paths --
+    one-workgroup deep-tail kernel, thread or wave paths --
     gives the layered oracle's bits (the schedule steers speed only)."""
     from opticalflowfromdepth_amd import _native, forward_warp_flow, ops, synth
     lib = _native.lib()
@@ -300,7 +328,7 @@ def test_layered_vs_sequential_divergence_on_warped_images():
 @pytest.fixture(autouse=True)
 def _no_fill_faults(request):
     """Every GPU hole-fill test ends with no invariant-violation bit raised
-    (ofd_inpaint_faults: a layered tail wait that gave up, a sequential bucket
+    (ofd_inpaint_faults: a sequential bucket
     or distance sweep past its bound); each would mean an incomplete fill."""
     yield
     if request.node.get_closest_marker("gpu") is not None and torch.cuda.is_available():
@@ -310,11 +338,11 @@ def _no_fill_faults(request):
 
 
 @pytest.mark.gpu
-def test_inpaint_tail_queue_beside_a_persistent_warp():
+def test_inpaint_tail_beside_a_persistent_warp():
     """The layered fill's deep-tail kernel (schedule (0, 0): every layer on it)
-    runs while the FW warp's persistent SPLAT holds CUs on another stream: its
-    ticket queue needs no co-resident grid, so the bits stay the
-    oracle's and no wait gives up."""
+    runs while the FW warp's persistent SPLAT holds CUs on another stream: it
+    is one workgroup that waits on no other (no co-residency
+    assumed), so the bits stay the oracle's."""
     from opticalflowfromdepth_amd import _native, forward_warp_flow, ops, synth
     lib = _native.lib()
     dev = torch.device("cuda:0")
