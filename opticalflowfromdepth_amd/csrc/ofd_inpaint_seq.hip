@@ -1563,7 +1563,7 @@ __global__ __launch_bounds__(256) void sq_record3_kernel(SqWs w) {
 }
 
 struct C3Lds {
-    uint32_t nnext;
+    uint32_t nnext[3];  // level l appends to nnext[l % 3]; reset two levels ahead (one barrier per level)
     uint64_t fr[2][kFrCap];
     float buf[kSlots3][kBufStride];  // per hole: the 9x9 colour grid (81 words), then the terms
     float res[kSlots3][9];       // per hole: chain results (Ia, Jx, Jy per channel)
@@ -1598,13 +1598,17 @@ __global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, int C, int H, 
     int cur = 0;
     uint32_t n = m.meta[2], levels = 0;
     for (uint32_t e = tid; e < n && e < uint32_t(kFrCap); e += 1024) L.fr[0][e] = ga[e];
-    if (tid == 0) L.nnext = 0u;
+    if (tid == 0) L.nnext[0] = 0u;
     __syncthreads();
-    const int nch = 3 * C;  // chains: (Ia, Jx, Jy) per channel
+    const int nch = 3 * C;
+    int lv = 0;  // chains: (Ia, Jx, Jy) per channel
     uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     (void)prof;
     while (n) {
         ++levels;
+        // the counter the next level appends to: last read right after the
+        // barrier that ended the level before the previous one
+        if (tid == 0) L.nnext[lv == 2 ? 0 : lv + 1] = 0u;
         SQ_T(l0);
         for (uint32_t base = 0; base < n; base += kSlots3) {
             if (base + uint32_t(tid / 64) * (64 / kL3) >= n) continue;  // no hole of this round in this wave
@@ -1747,7 +1751,7 @@ __global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, int C, int H, 
 #pragma unroll
             for (int k = 0; k < 8; ++k)
                 if ((old[k] & 63u) == 1u) {
-                    const uint32_t f = atomicAdd(&L.nnext, 1u);
+                    const uint32_t f = atomicAdd(&L.nnext[lv], 1u);
                     const int64_t q = int64_t(p) + int64_t(WC(k) / 9 - 4) * ew + (WC(k) % 9 - 4);
                     const uint64_t en = (uint64_t(old[k] >> 6) << 32) | uint64_t(q);
                     if (f < uint32_t(kFrCap))
@@ -1770,14 +1774,15 @@ __global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, int C, int H, 
         SQ_T(l2);
         SQ_ACC(0, l0, l1);
         SQ_ACC(1, l1, l2);
-        n = L.nnext;
-        __syncthreads();
-        if (tid == 0) L.nnext = 0u;
+        // one barrier per level: the next level writes the frontier buffer
+        // and counter this one read (all reads done before the barrier) and
+        // appends to a counter zeroed before it
+        n = L.nnext[lv];
+        lv = lv == 2 ? 0 : lv + 1;
         cur ^= 1;
         uint64_t *tmp = ga;
         ga = gb;
         gb = tmp;
-        __syncthreads();
     }
     if (tid == 0) {
         m.meta[3] = levels;
