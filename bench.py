@@ -445,7 +445,7 @@ def rank_report(ms_per_step: float, world: int, coll_dev) -> dict:
     """What the process group saw: its size (dist.get_world_size(), not the
     launcher's WORLD_SIZE), its backend, and every rank's own ms per step
     (all_gather; the line's ms_per_step is the max-rank wall clock)."""
-    if world <= 1 or not dist.is_initialized():
+    if not dist.is_initialized():
         return {"world_size": 1, "backend": None, "ms_per_step": [round(ms_per_step, 4)]}
     n = dist.get_world_size()
     mine = torch.tensor([ms_per_step], dtype=torch.float64, device=coll_dev)
@@ -458,7 +458,7 @@ def finish(world: int) -> None:
     """Final barrier, then teardown: rank 0 runs its extra phases after the
     timed steps, and no rank may tear the process group down while another
     still uses it."""
-    if world > 1 and dist.is_initialized():
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 
@@ -523,7 +523,10 @@ def main(argv=None):
     gpu = 0 if os.environ.get("OFD_BENCH_SAME_DEVICE") == "1" else local
     dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
-    if world > 1:
+    # a process group whenever a launcher started this process (WORLD_SIZE set),
+    # so `torchrun --nproc-per-node 1 bench.py` runs the RCCL path at one rank
+    pg = world > 1 or "WORLD_SIZE" in os.environ
+    if pg:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -563,7 +566,7 @@ def main(argv=None):
         ev.record(stream)
     torch.cuda.synchronize()
     lib = _native.lib()
-    if world > 1:
+    if pg:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -590,7 +593,7 @@ def main(argv=None):
         if evmode >= 2:
             ends[k].record(stream)
     torch.cuda.synchronize()
-    if world > 1:
+    if pg:
         dist.barrier()
     wall = time.perf_counter() - t0
     lib.ofd_fw_set_profile_events(None, None)
@@ -601,7 +604,7 @@ def main(argv=None):
 
     ranks = rank_report(wall / args.steps * 1e3, world, coll_dev)
     t = torch.tensor([wall, dev_ms], dtype=torch.float64, device=coll_dev)
-    if world > 1:
+    if pg:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall, dev_ms_max = float(t[0]), float(t[1])
 

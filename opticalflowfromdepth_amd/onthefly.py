@@ -225,11 +225,13 @@ def main(argv: Optional[Sequence[str]] = None):
     local = int(os.environ.get("LOCAL_RANK", 0))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    # DDP over RCCL whenever a launcher started this process (one rank included)
+    pg = world > 1 or "WORLD_SIZE" in os.environ
+    if pg:
         dist.init_process_group("nccl", device_id=dev)
     torch.manual_seed(0)
     model = IterativeFlowNet().to(dev)
-    if world > 1:
+    if pg:
         model = nn.parallel.DistributedDataParallel(model, device_ids=[local])
     opt, sched = fetch_optimizer(model, num_steps=a.steps + a.warmup)
     h, w = a.size
@@ -241,13 +243,13 @@ def main(argv: Optional[Sequence[str]] = None):
     for b in batches[:a.warmup]:
         train_step(model, opt, sched, b, dev, args)
     torch.cuda.synchronize()
-    if world > 1:
+    if pg:
         dist.barrier()
     t0 = time.perf_counter()
     for b in batches[a.warmup:]:
         loss, m = train_step(model, opt, sched, b, dev, args)
     torch.cuda.synchronize()
-    if world > 1:
+    if pg:
         dist.barrier()
     el = torch.tensor([time.perf_counter() - t0], device=dev)
     # the pair builder alone over the same (device-resident) batches
@@ -258,7 +260,7 @@ def main(argv: Optional[Sequence[str]] = None):
         make_pairs(*b)
     torch.cuda.synchronize()
     el_pairs = time.perf_counter() - t1
-    if world > 1:
+    if pg:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     if rank == 0:
         pairs = a.steps * a.batch * world
@@ -267,7 +269,7 @@ def main(argv: Optional[Sequence[str]] = None):
                           "pairs_ms_per_step": el_pairs / a.steps * 1e3,
                           "loss": float(loss), "epe": float(m["epe"]), "config": {"size": [h, w],
                                                                                    "batch_per_rank": a.batch}}))
-    if world > 1:
+    if pg:
         dist.destroy_process_group()
 
 

