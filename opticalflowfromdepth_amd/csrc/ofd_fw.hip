@@ -1531,6 +1531,66 @@ unsigned persist_grid(unsigned tiles) {
     return tiles < slots ? tiles : slots;
 }
 
+// ---- Two-stream schedule of one chunk (ofd_fw_set_pipeline, OFD_FW_PIPE).
+// The chunk's images are cut into halves A and B, each with its own BIN,
+// persistent SPLAT and queue words:
+//     caller stream : BIN(A) -> [fork] -> SPLAT(A) ------------------> [wait join]
+//     helper stream :           [wait fork] -> BIN(B) -> SPLAT(B) -> [join]
+// BIN(B) streams the second half's flow while SPLAT(A)'s latency-bound scans
+// leave HBM idle, and SPLAT(B)'s workgroups take the slots SPLAT(A)'s drain
+// frees (two persistent grids, one pool of slots), so only BIN(A) and one
+// drain stay on the critical path.  Results are bit-identical either way:
+// the halves touch disjoint images and workspace slabs.
+int g_pipe = -1;
+bool pipe_enabled() {
+    if (g_pipe < 0) {
+        const char *e = getenv("OFD_FW_PIPE");
+        g_pipe = e ? atoi(e) : 0;
+    }
+    return g_pipe > 0;
+}
+
+struct PipeRes {
+    hipStream_t helper = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+std::mutex g_pipe_mu;  // held while a call enqueues its fork / join (shared events)
+PipeRes g_pipe_res[64];
+
+// the device's helper stream and events (created on first use), or nullptr
+PipeRes *pipe_res() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    PipeRes &r = g_pipe_res[dev];
+    if (!r.helper) {
+        hipStream_t s = nullptr;
+        hipEvent_t f = nullptr, j = nullptr;
+        if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+        if (hipEventCreateWithFlags(&f, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&j, hipEventDisableTiming) != hipSuccess) {
+            (void)hipStreamDestroy(s);
+            return nullptr;
+        }
+        r.fork = f;
+        r.join = j;
+        r.helper = s;
+    }
+    return &r;
+}
+
+// The workspace views of images [h, ...) of a chunk slab, with the second
+// queue block (16 words past the first, inside the per-image slack).
+Ws offset_ws(const Ws &w, int64_t h, int64_t HW, const TileGeom &g) {
+    Ws o = w;
+    o.keys += h * HW;
+    o.winner += h * HW;
+    o.flag += h * g.ntiles;
+    o.segrec += h * g.nseg;
+    o.blkrec += h * g.nsb;
+    o.queue += 16;
+    return o;
+}
+
 // Optional timing hook (ofd_fw_set_profile_events): events recorded on the
 // launch stream right before the first and right after the last RESOLVE
 // launch of a call -- the dominant kernel -- so a benchmark can time it with
@@ -1586,6 +1646,53 @@ int run_f32(Coords co, const E *obj, const float *depth, E *out, float *valid, f
                 hipLaunchKernelGGL(resolve_atomic_kernel, dim3(grid_for(px, kBlock * 4)), dim3(kBlock), 0, st,
                                    obj, slab.keys, out, valid, coll, int(C), HW, b0, px);
                 if (c == nch - 1 && g_prof_stop) (void)hipEventRecord(g_prof_stop, st);
+                continue;
+            }
+        }
+        if (mode == Mode::Tile && nch == 1 && nb >= 2 && pipe_enabled()) {
+            hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+            PipeRes *pr = hipStreamIsCapturing(st, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone
+                              ? pipe_res() : nullptr;
+            if (pr) {
+                const SplatIO io{valid, coll, obj, out, int(C), int(C) - Coords::kGen, gen_at};
+                const int64_t h = nb / 2;
+                const ChunkArgs aA{slab, b0, int(h)};
+                const ChunkArgs aB{offset_ws(slab, h, HW, g), b0 + h, int(nb - h)};
+                using Cfg = FusedCfgFor<Coords>;
+                auto bin = [&](const ChunkArgs &a, hipStream_t s) {
+                    const dim3 bgrid(grid_for(int64_t(a.nimg) * g.nseg, kWaves * kBinSPW));
+                    if (vec)
+                        hipLaunchKernelGGL((bin_kernel<Coords, true, kBinSPW>), bgrid, dim3(kWarpThreads), 0, s, co,
+                                           depth, a, int(H), int(W), HW, g);
+                    else
+                        hipLaunchKernelGGL((bin_kernel<Coords, false, kBinSPW>), bgrid, dim3(kWarpThreads), 0, s, co,
+                                           depth, a, int(H), int(W), HW, g);
+                };
+                auto splat = [&](const ChunkArgs &a, hipStream_t s) {
+                    const unsigned tiles = unsigned(a.nimg) * unsigned(g.ntiles);
+                    if (vec)
+                        hipLaunchKernelGGL((splat_persist_kernel<Coords, true, true, false, Cfg, E>),
+                                           dim3(persist_grid<Coords, true, Cfg, E>(tiles)), dim3(Cfg::kThr), 0, s, co,
+                                           depth, io, a, int(H), int(W), HW, g, nullptr);
+                    else
+                        hipLaunchKernelGGL((splat_persist_kernel<Coords, false, true, false, Cfg, E>),
+                                           dim3(persist_grid<Coords, false, Cfg, E>(tiles)), dim3(Cfg::kThr), 0, s,
+                                           co, depth, io, a, int(H), int(W), HW, g, nullptr);
+                };
+                std::lock_guard<std::mutex> lk(g_pipe_mu);
+                bin(aA, st);
+                hipError_t e = hipEventRecord(pr->fork, st);
+                if (e == hipSuccess) e = hipStreamWaitEvent(pr->helper, pr->fork, 0);
+                if (e != hipSuccess) return int(e);
+                if (g_prof_start) (void)hipEventRecord(g_prof_start, st);
+                splat(aA, st);
+                bin(aB, pr->helper);
+                if (g_pipe == 1) splat(aB, pr->helper);  // probe 2: SPLAT(B) after SPLAT(A) on the caller's stream
+                e = hipEventRecord(pr->join, pr->helper);
+                if (e == hipSuccess) e = hipStreamWaitEvent(st, pr->join, 0);
+                if (e != hipSuccess) return int(e);
+                if (g_pipe != 1) splat(aB, st);
+                if (g_prof_stop) (void)hipEventRecord(g_prof_stop, st);
                 continue;
             }
         }
@@ -1773,6 +1880,12 @@ int ofd_fw_set_profile_events(void *start_event, void *stop_event) {
 int ofd_fw_set_disparity_rows(int on) {
     const int prev = disp_row_enabled() ? 1 : 0;
     if (on == 0 || on == 1) g_disp_rows = on;
+    return prev;
+}
+
+int ofd_fw_set_pipeline(int on) {
+    const int prev = pipe_enabled() ? g_pipe : 0;
+    if (on == 0 || on == 1 || on == 2) g_pipe = on;
     return prev;
 }
 
