@@ -94,15 +94,6 @@ int ofd_fw_set_engine(int engine);
  * queries.  Returns the previous setting.  Process-wide, not thread-safe. */
 int ofd_fw_set_disparity_rows(int on);
 
-/* TILE engine, one chunk of two or more images: on = 1 runs the second half
- * of the images on a library-owned helper stream (its BIN overlaps the first
- * half's SPLAT; the call's stream waits for it before returning, so stream
- * order for the caller is unchanged; not used while the stream is being
- * captured); on = 0 runs every launch on the call's stream.  Results are
- * identical.  Also OFD_FW_PIPE=0/1; any other value only queries.  Returns the
- * previous setting.  Process-wide, not thread-safe. */
-int ofd_fw_set_pipeline(int on);
-
 /* Benchmark hook: when non-NULL, the given hipEvent_t's are recorded on the
  * launch stream right before the first and right after the last launch of
  * each subsequent f32 call's dominant kernel: SPLAT (TILE engine), RESOLVE

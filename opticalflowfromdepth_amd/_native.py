@@ -33,7 +33,6 @@ SIGNATURES = {
     "ofd_fw_strerror": ([ctypes.c_int], ctypes.c_char_p),
     "ofd_fw_set_engine": ([ctypes.c_int], ctypes.c_int),
     "ofd_fw_set_disparity_rows": ([ctypes.c_int], ctypes.c_int),
-    "ofd_fw_set_pipeline": ([ctypes.c_int], ctypes.c_int),
     "ofd_fw_set_profile_events": ([_P, _P], ctypes.c_int),
     "ofd_fw_workspace_bytes": ([_I64, _I64, _I64, ctypes.c_int], _SZ),
     "ofd_fw_workspace_init": ([_P, _SZ, _P], ctypes.c_int),

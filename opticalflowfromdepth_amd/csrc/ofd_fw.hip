@@ -75,6 +75,9 @@ constexpr int SBW = 16, SBH = 4;          // source block = one wave (64 px)
 constexpr int SEGB = 8;                   // source blocks per segment (128 x 4 px)
 constexpr int MAX_TILES_PER_BLOCK = 12;   // wider boxes go through the global path
 constexpr int kSplatU = 2;                // 4-block slots in flight per wave (SPLAT, f32 coords; 3 spills)
+#ifndef OFD_BIN_MINW  // BIN waves per SIMD the register budget must allow (probe builds override)
+#define OFD_BIN_MINW 8
+#endif
 constexpr int kBinSPW = 1;                // segments per BIN wave (bin_kernel; 2 measured slower, also for depth-only sources)
 
 
@@ -771,8 +774,22 @@ __device__ __forceinline__ void bin_segment(const Coords &co, const float *__res
 // kSPW segments per wave (consecutive in the image's segment order): every
 // segment's coordinate loads are issued before the first one is folded
 // (2 / 4: 0.754 / 0.763 ms per 64-image step vs 0.737 at 1).
+// BIN's register budget: 8 waves per SIMD (<= 64 VGPRs) for the float
+// coordinate sources, which fit it without spilling (66 -> 64 VGPRs lifts BIN
+// from 3 to 4 workgroups per CU, no measurable change in time: BIN streams at
+// ~5.6 TB/s either way); the double and ego-motion sources keep the
+// compiler's own choice (they would spill).
+template <typename C>
+struct BinMinW {
+    static constexpr int value = sizeof(typename C::V) == 4 ? OFD_BIN_MINW : 1;
+};
+template <typename D>
+struct BinMinW<EgoCoords<D>> {
+    static constexpr int value = 1;
+};
+
 template <typename Coords, bool kVec, int kSPW = 1>
-__global__ __launch_bounds__(kWarpThreads) void bin_kernel(Coords co, const float *__restrict__ depth, ChunkArgs a,
+__global__ __launch_bounds__(kWarpThreads, BinMinW<Coords>::value) void bin_kernel(Coords co, const float *__restrict__ depth, ChunkArgs a,
                                                               int H, int W, int64_t HW, TileGeom g) {
     using V = typename Coords::V;
     const int lane = lane_id();
@@ -1226,7 +1243,13 @@ using SplitCfg = SplatCfg<512, 2, 8>;  // split engine: 4 workgroups / CU, light
 #define OFD_PROBE_THR 512
 #define OFD_PROBE_MINW 4
 #endif
-using FusedCfg = SplatCfg<OFD_PROBE_THR, 8, OFD_PROBE_MINW>;
+#ifndef OFD_PROBE_GT  // targets in flight per thread in the publish (probe builds override)
+#define OFD_PROBE_GT 8
+#endif
+#ifndef OFD_PROBE_UF  // 4-block splat slots in flight per wave (probe builds override)
+#define OFD_PROBE_UF kSplatU
+#endif
+using FusedCfg = SplatCfg<OFD_PROBE_THR, OFD_PROBE_GT, OFD_PROBE_MINW, OFD_PROBE_UF>;
 // coordinate sources that generate channels carry the generated values and a
 // division per source: 4 targets in flight keeps them inside 128 VGPRs
 // (Coords::kGenGT of them: 4 for the disparity source, 2 for the ego-motion
@@ -1531,66 +1554,6 @@ unsigned persist_grid(unsigned tiles) {
     return tiles < slots ? tiles : slots;
 }
 
-// ---- Two-stream schedule of one chunk (ofd_fw_set_pipeline, OFD_FW_PIPE).
-// The chunk's images are cut into halves A and B, each with its own BIN,
-// persistent SPLAT and queue words:
-//     caller stream : BIN(A) -> [fork] -> SPLAT(A) ------------------> [wait join]
-//     helper stream :           [wait fork] -> BIN(B) -> SPLAT(B) -> [join]
-// BIN(B) streams the second half's flow while SPLAT(A)'s latency-bound scans
-// leave HBM idle, and SPLAT(B)'s workgroups take the slots SPLAT(A)'s drain
-// frees (two persistent grids, one pool of slots), so only BIN(A) and one
-// drain stay on the critical path.  Results are bit-identical either way:
-// the halves touch disjoint images and workspace slabs.
-int g_pipe = -1;
-bool pipe_enabled() {
-    if (g_pipe < 0) {
-        const char *e = getenv("OFD_FW_PIPE");
-        g_pipe = e ? atoi(e) : 0;
-    }
-    return g_pipe > 0;
-}
-
-struct PipeRes {
-    hipStream_t helper = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
-};
-std::mutex g_pipe_mu;  // held while a call enqueues its fork / join (shared events)
-PipeRes g_pipe_res[64];
-
-// the device's helper stream and events (created on first use), or nullptr
-PipeRes *pipe_res() {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-    PipeRes &r = g_pipe_res[dev];
-    if (!r.helper) {
-        hipStream_t s = nullptr;
-        hipEvent_t f = nullptr, j = nullptr;
-        if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
-        if (hipEventCreateWithFlags(&f, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&j, hipEventDisableTiming) != hipSuccess) {
-            (void)hipStreamDestroy(s);
-            return nullptr;
-        }
-        r.fork = f;
-        r.join = j;
-        r.helper = s;
-    }
-    return &r;
-}
-
-// The workspace views of images [h, ...) of a chunk slab, with the second
-// queue block (16 words past the first, inside the per-image slack).
-Ws offset_ws(const Ws &w, int64_t h, int64_t HW, const TileGeom &g) {
-    Ws o = w;
-    o.keys += h * HW;
-    o.winner += h * HW;
-    o.flag += h * g.ntiles;
-    o.segrec += h * g.nseg;
-    o.blkrec += h * g.nsb;
-    o.queue += 16;
-    return o;
-}
-
 // Optional timing hook (ofd_fw_set_profile_events): events recorded on the
 // launch stream right before the first and right after the last RESOLVE
 // launch of a call -- the dominant kernel -- so a benchmark can time it with
@@ -1646,53 +1609,6 @@ int run_f32(Coords co, const E *obj, const float *depth, E *out, float *valid, f
                 hipLaunchKernelGGL(resolve_atomic_kernel, dim3(grid_for(px, kBlock * 4)), dim3(kBlock), 0, st,
                                    obj, slab.keys, out, valid, coll, int(C), HW, b0, px);
                 if (c == nch - 1 && g_prof_stop) (void)hipEventRecord(g_prof_stop, st);
-                continue;
-            }
-        }
-        if (mode == Mode::Tile && nch == 1 && nb >= 2 && pipe_enabled()) {
-            hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-            PipeRes *pr = hipStreamIsCapturing(st, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone
-                              ? pipe_res() : nullptr;
-            if (pr) {
-                const SplatIO io{valid, coll, obj, out, int(C), int(C) - Coords::kGen, gen_at};
-                const int64_t h = nb / 2;
-                const ChunkArgs aA{slab, b0, int(h)};
-                const ChunkArgs aB{offset_ws(slab, h, HW, g), b0 + h, int(nb - h)};
-                using Cfg = FusedCfgFor<Coords>;
-                auto bin = [&](const ChunkArgs &a, hipStream_t s) {
-                    const dim3 bgrid(grid_for(int64_t(a.nimg) * g.nseg, kWaves * kBinSPW));
-                    if (vec)
-                        hipLaunchKernelGGL((bin_kernel<Coords, true, kBinSPW>), bgrid, dim3(kWarpThreads), 0, s, co,
-                                           depth, a, int(H), int(W), HW, g);
-                    else
-                        hipLaunchKernelGGL((bin_kernel<Coords, false, kBinSPW>), bgrid, dim3(kWarpThreads), 0, s, co,
-                                           depth, a, int(H), int(W), HW, g);
-                };
-                auto splat = [&](const ChunkArgs &a, hipStream_t s) {
-                    const unsigned tiles = unsigned(a.nimg) * unsigned(g.ntiles);
-                    if (vec)
-                        hipLaunchKernelGGL((splat_persist_kernel<Coords, true, true, false, Cfg, E>),
-                                           dim3(persist_grid<Coords, true, Cfg, E>(tiles)), dim3(Cfg::kThr), 0, s, co,
-                                           depth, io, a, int(H), int(W), HW, g, nullptr);
-                    else
-                        hipLaunchKernelGGL((splat_persist_kernel<Coords, false, true, false, Cfg, E>),
-                                           dim3(persist_grid<Coords, false, Cfg, E>(tiles)), dim3(Cfg::kThr), 0, s,
-                                           co, depth, io, a, int(H), int(W), HW, g, nullptr);
-                };
-                std::lock_guard<std::mutex> lk(g_pipe_mu);
-                bin(aA, st);
-                hipError_t e = hipEventRecord(pr->fork, st);
-                if (e == hipSuccess) e = hipStreamWaitEvent(pr->helper, pr->fork, 0);
-                if (e != hipSuccess) return int(e);
-                if (g_prof_start) (void)hipEventRecord(g_prof_start, st);
-                splat(aA, st);
-                bin(aB, pr->helper);
-                if (g_pipe == 1) splat(aB, pr->helper);  // probe 2: SPLAT(B) after SPLAT(A) on the caller's stream
-                e = hipEventRecord(pr->join, pr->helper);
-                if (e == hipSuccess) e = hipStreamWaitEvent(st, pr->join, 0);
-                if (e != hipSuccess) return int(e);
-                if (g_pipe != 1) splat(aB, st);
-                if (g_prof_stop) (void)hipEventRecord(g_prof_stop, st);
                 continue;
             }
         }
@@ -1880,12 +1796,6 @@ int ofd_fw_set_profile_events(void *start_event, void *stop_event) {
 int ofd_fw_set_disparity_rows(int on) {
     const int prev = disp_row_enabled() ? 1 : 0;
     if (on == 0 || on == 1) g_disp_rows = on;
-    return prev;
-}
-
-int ofd_fw_set_pipeline(int on) {
-    const int prev = pipe_enabled() ? g_pipe : 0;
-    if (on == 0 || on == 1 || on == 2) g_pipe = on;
     return prev;
 }
 

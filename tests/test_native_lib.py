@@ -76,17 +76,6 @@ def test_disparity_rows_switch():
     lib.ofd_fw_set_disparity_rows(cur)
 
 
-def test_pipeline_switch():
-    from opticalflowfromdepth_amd import _native
-    lib = _native.lib()
-    cur = lib.ofd_fw_set_pipeline(-1)
-    assert cur in (0, 1)
-    assert lib.ofd_fw_set_pipeline(0) == cur
-    assert lib.ofd_fw_set_pipeline(1) == 0
-    assert lib.ofd_fw_set_pipeline(-1) == 1
-    lib.ofd_fw_set_pipeline(cur)
-
-
 def test_argument_errors_without_gpu():
     """Validation happens before any HIP call, so it is testable on CPU."""
     from opticalflowfromdepth_amd import _native

@@ -6,12 +6,13 @@
 #   tools/seq_probe.sh run [B]    (GPU box)
 set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
-OUT="$R/tools/_probe/libofd_fw_sqprof.so"
+OUT="$R/opticalflowfromdepth_amd/_build/libofd_fw_sqprof.so"
 if [ "$1" = build ]; then
-  mkdir -p "$R/tools/_probe"
+  mkdir -p "$(dirname "$OUT")"
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -DOFD_SQ_PROF \
     -I "$R/include" -o "$OUT" "$R"/opticalflowfromdepth_amd/csrc/ofd_fw.hip \
-    "$R"/opticalflowfromdepth_amd/csrc/ofd_inpaint.hip "$R"/opticalflowfromdepth_amd/csrc/ofd_inpaint_seq.hip
+    "$R"/opticalflowfromdepth_amd/csrc/ofd_inpaint.hip "$R"/opticalflowfromdepth_amd/csrc/ofd_inpaint_seq.hip \
+    "$R"/opticalflowfromdepth_amd/csrc/ofd_deflate.hip
 else
   OFD_FW_LIB="$OUT" python3 -u "$R/tools/seq_time.py" "${2:-16}"
 fi

@@ -66,6 +66,14 @@ def main():
             print("COLOUR3 level work/barrier, per-round loads/terms/chains/final+append/atomics (Mclk):",
                   [round(x * 256 / 1e6, 2) for x in r[16:23]])
         print("max levels", m[:, 3].max(), "max buckets", m[:, 4].max(), "errors", int((m[:, 5] != 0).sum()))
+        if m[:, 8:24].any():  # per image: FMM phase sum vs COLOUR3 level work + barrier (Mclk)
+            f = m[:, 8:14].astype(np.float64).sum(1) * 256 / 1e6
+            c = m[:, 16:18].astype(np.float64).sum(1) * 256 / 1e6
+            print("per image (Mclk): max FMM", round(f.max(), 2), "max COLOUR3", round(c.max(), 2),
+                  "max FMM+COLOUR3", round((f + c).max(), 2))
+            for k in np.argsort(-(f + c))[:6]:
+                print("  image", int(k), "FMM", round(f[k], 2), "COLOUR3", round(c[k], 2), "levels", int(m[k, 3]),
+                      "buckets", int(m[k, 4]), "pushes", int(m[k, 1]))
         return
     lsz = ws[k1 + kdeep * en * 8: k1 + kdeep * en * 8 + L * 4].view(torch.int32).cpu().numpy()
     q = np.percentile(lsz, [0, 10, 50, 90, 99, 100])
