@@ -105,7 +105,7 @@ struct SqWs {
     uint64_t *k1;
     uint32_t *rowc;  // band count / offset per padded row
     uint32_t *meta;  // kMeta words per image
-    uint32_t *rec;   // radius-3 COLOUR: kRecW words per hole, indexed by push seq - band count
+    uint32_t *rec;   // radius-3 COLOUR: kRecW words per hole, indexed by padded pixel
     uint32_t *shd;   // radius-3 COLOUR: the image as packed uint8 channels (C <= 3), H x W words
     uint64_t *fr2;   // radius-3 COLOUR: second frontier buffer (entries beyond the LDS capacity)
     int64_t en, eh, ew, hw;
@@ -1491,7 +1491,9 @@ __global__ __launch_bounds__(256) void sq_record3_kernel(SqWs w) {
     auto TT = [&](int y, int x) -> float { return Lt[y - i0][x - j0]; };
     const uint32_t s = Ls[li][lj];
     if (s == 0u || s == INF) return;
-    const uint32_t idx = s - m.meta[0];
+    // records are indexed by padded pixel (the region holds en records), so
+    // COLOUR3 can address a dependant's record without a lookup
+    const uint32_t idx = uint32_t(p);
     // Kahn counter and dependants: window positions inside the image (the
     // tile's clamped halo holds the image's own pixels there)
     uint32_t cnt = 0;
@@ -1558,7 +1560,7 @@ __global__ __launch_bounds__(256) void sq_record3_kernel(SqWs w) {
     uint4 *dstp = reinterpret_cast<uint4 *>(m.rec + size_t(idx) * kRecW);
 #pragma unroll
     for (int k = 0; k < kRecW / 4; ++k) dstp[k] = make_uint4(r[4 * k], r[4 * k + 1], r[4 * k + 2], r[4 * k + 3]);
-    m.own[p] = (idx << 6) | cnt;  // cnt <= 60; idx < 2^26 (the launcher's bound)
+    m.own[p] = (idx << 6) | cnt;  // cnt <= 60; idx = p < en < 2^26 (the launcher's bound)
     if (cnt == 0u) m.k0[atomicAdd(&m.meta[2], 1u)] = (uint64_t(idx) << 32) | uint64_t(p);
 }
 
