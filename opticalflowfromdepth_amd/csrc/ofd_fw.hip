@@ -1259,7 +1259,14 @@ using FusedGenCfg = SplatCfg<512, Coords::kGenGT, 4>;
 template <typename Coords>
 using FusedCfgFor = typename std::conditional<Coords::kGen == 0, FusedCfg, FusedGenCfg<Coords>>::type;
 
-template <typename Coords, bool kVec, bool kFuse = false, bool kStamp = false, typename Cfg = SplitCfg>
+// One workgroup per tile (grid = the chunk's tiles, rounded up to 8): tile
+// lin = (blockIdx % 8) * per + blockIdx / 8, so the workgroups of one XCD
+// (round-robin placement) take consecutive tiles of the band-major order.
+// The fused TILE engine uses it for calls of few tiles per resident slot,
+// where the hardware's dispatch of fresh workgroups balances the last tiles
+// better than the persistent kernel's queues (see run_f32).
+template <typename Coords, bool kVec, bool kFuse = false, bool kStamp = false, typename Cfg = SplitCfg,
+          typename E = float>
 __global__ __launch_bounds__(Cfg::kThr, Cfg::kMinW) void splat_kernel(Coords co, const float *__restrict__ depth,
                                                                 SplatIO io, ChunkArgs a, int H, int W, int64_t HW,
                                                                 TileGeom g, unsigned long long *stamps = nullptr) {
@@ -1270,7 +1277,7 @@ __global__ __launch_bounds__(Cfg::kThr, Cfg::kMinW) void splat_kernel(Coords co,
     if (lin >= total) return;
     int bl, tile;
     tile_of<Cfg>(lin, a, g, bl, tile);
-    splat_tile<Coords, kVec, kFuse, kStamp, Cfg>(L, lin, bl, tile, co, depth, io, a, H, W, HW, g, stamps);
+    splat_tile<Coords, kVec, kFuse, kStamp, Cfg, E>(L, lin, bl, tile, co, depth, io, a, H, W, HW, g, stamps);
 }
 
 // Persistent SPLAT: one workgroup per resident slot, looping over tiles.  The
@@ -1549,9 +1556,30 @@ unsigned resident_slots(K kernel, int threads) {
 }
 
 template <typename Coords, bool kVec, typename Cfg = FusedCfgFor<Coords>, typename E = float>
-unsigned persist_grid(unsigned tiles) {
+unsigned persist_slots() {
     static const unsigned slots = resident_slots(splat_persist_kernel<Coords, kVec, true, false, Cfg, E>, Cfg::kThr);
+    return slots;
+}
+
+template <typename Coords, bool kVec, typename Cfg = FusedCfgFor<Coords>, typename E = float>
+unsigned persist_grid(unsigned tiles) {
+    const unsigned slots = persist_slots<Coords, kVec, Cfg, E>();
     return tiles < slots ? tiles : slots;
+}
+
+// Calls with fewer than persist_min() tiles per resident SPLAT slot launch
+// one workgroup per tile instead of the persistent kernel (OFD_PERSIST_MIN
+// overrides; 0 = always persistent).  Whole calls (tools/ab_env.sh, ms):
+// config 2 (32 x 480x640, 4.7 tiles per slot) 0.156 one-per-tile vs 0.184
+// persistent; config 5 (64 x 368x560, 7.5) 0.218 vs 0.234; 32 x 768x1024 (12)
+// 0.383 vs 0.387; 16 x 768x1024 (6) 0.218 vs 0.216; the headline (24) 0.741
+// vs 0.721 -- the persistent queues pay off only on long calls.
+unsigned persist_min() {
+    static const unsigned v = [] {
+        const char *e = getenv("OFD_PERSIST_MIN");
+        return e ? unsigned(atoi(e)) : 16u;
+    }();
+    return v;
 }
 
 // Optional timing hook (ofd_fw_set_profile_events): events recorded on the
@@ -1628,7 +1656,16 @@ int run_f32(Coords co, const E *obj, const float *depth, E *out, float *valid, f
                 const unsigned tiles = unsigned(nb * g.ntiles);
                 if (c == 0 && g_prof_start) (void)hipEventRecord(g_prof_start, st);
                 using Cfg = FusedCfgFor<Coords>;
-                if (vec)
+                const bool per_tile = vec ? tiles < persist_min() * persist_slots<Coords, true, Cfg, E>()
+                                          : tiles < persist_min() * persist_slots<Coords, false, Cfg, E>();
+                if (per_tile) {
+                    if (vec)
+                        hipLaunchKernelGGL((splat_kernel<Coords, true, true, false, Cfg, E>), sgrid, dim3(Cfg::kThr),
+                                           0, st, co, depth, io, a, int(H), int(W), HW, g, nullptr);
+                    else
+                        hipLaunchKernelGGL((splat_kernel<Coords, false, true, false, Cfg, E>), sgrid, dim3(Cfg::kThr),
+                                           0, st, co, depth, io, a, int(H), int(W), HW, g, nullptr);
+                } else if (vec)
                     hipLaunchKernelGGL((splat_persist_kernel<Coords, true, true, false, Cfg, E>),
                                        dim3(persist_grid<Coords, true, Cfg, E>(tiles)), dim3(Cfg::kThr), 0, st, co, depth, io,
                                        a, int(H), int(W), HW, g, nullptr);

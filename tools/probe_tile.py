@@ -64,7 +64,7 @@ def main():
     lib.probe_slab_bytes.argtypes = [I64] * 3
     lib.probe_slab_bytes.restype = ctypes.c_size_t
     dev = torch.device("cuda:0")
-    B, H, W = int(os.environ.get("B", "64")), 768, 1024
+    B, H, W = int(os.environ.get("B", "64")), int(os.environ.get("H", "768")), int(os.environ.get("W", "1024"))
     obj, flow, depth = synth.stage_one_batch([12345 + i for i in range(B)], H, W, dev,
                                              ego_fraction=float(os.environ.get("EGO", "0.5")))
     C = obj.shape[1]
