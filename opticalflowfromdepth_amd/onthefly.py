@@ -1,5 +1,5 @@
-"""On-the-fly training pairs inside a RAFT-style train loop (SURVEY.md 8(d)
-config 5, 8(f) rank 4; BASELINE.json configs[4]).
+"""On-the-fly training pairs inside a RAFT-style or GMFlow-style train loop
+(BASELINE.json configs[4]).
 
 The reference trains on pairs preprocess.py wrote to npz beforehand:
 adjusted_RAFT/train.py:184-211 pulls (image1, image2, flow, ..., valid) from a
@@ -20,7 +20,9 @@ hole-fill (ops.inpaint), then the step of train.py:185-211 under
 DistributedDataParallel over RCCL (one process per GPU, torchrun env) instead
 of DataParallel.  The flow network is a small stand-in with RAFT's interface
 (model(image1, image2, iters) -> list of full-resolution flows); RAFT itself is
-out of scope.
+out of scope.  The GMFlow loop (adjusted_gmflow/main.py:450-494)
+is ``gmflow_train_step`` with ``flow_loss_func`` (adjusted_gmflow/loss.py) and
+a global-matching stand-in, ``GlobalMatchFlowNet`` (``--arch gmflow``).
 
 ``PairOps`` carries the three device ops; the CPU multi-rank test
 (tests/test_onthefly.py) swaps in the CPU restatements kept under oracle/, the product
@@ -206,6 +208,105 @@ def shard_loader(n_images, h, w, batch, rank, world, base=0, workers=0):
                                        num_workers=workers, drop_last=True)
 
 
+# ---------------------------------------------------------------- GMFlow-style step
+# adjusted_gmflow/main.py:450-494 trains GMFlow on the same npz pairs with its
+# own loss (adjusted_gmflow/loss.py:4-37), AdamW(lr 4e-4, weight decay 1e-4,
+# :230-231), a cosine OneCycleLR over num_steps + 10 (:425-432), clip 1.0
+# (:51, :489), and skips a step whose loss is NaN (:479-480).  GMFlow itself is
+# out of scope like RAFT; the stand-in below has its forward contract
+# (model(img1, img2, attn_splits_list, corr_radius_list, prop_radius_list) ->
+# {'flow_preds': [...]}) and its core operation, global matching.
+GMFLOW_MAX_FLOW = 400  # adjusted_gmflow/main.py:39
+
+
+def flow_loss_func(flow_preds, flow_gt, valid, gamma=0.9, max_flow=GMFLOW_MAX_FLOW):
+    """adjusted_gmflow/loss.py:4-37: gamma-weighted L1 over the predictions on
+    valid pixels with |flow| < max_flow; metrics count epe ABOVE 1 / 3 / 5 px
+    (RAFT's sequence_loss counts below).  Metrics stay tensors (no host sync)."""
+    n = len(flow_preds)
+    mag = torch.sum(flow_gt ** 2, dim=1).sqrt()
+    valid = (valid >= 0.5) & (mag < max_flow)
+    loss = 0.0
+    for i in range(n):
+        w = gamma ** (n - i - 1)
+        loss = loss + w * (valid[:, None] * (flow_preds[i].float() - flow_gt).abs()).mean()
+    epe = torch.sum((flow_preds[-1].float() - flow_gt) ** 2, dim=1).sqrt().view(-1)[valid.view(-1)]
+    return loss, {"epe": epe.mean(), "1px": (epe > 1).float().mean(), "3px": (epe > 3).float().mean(),
+                  "5px": (epe > 5).float().mean()}
+
+
+class GlobalMatchFlowNet(nn.Module):
+    """A small GMFlow-shaped network: features at 1/8 resolution, global
+    matching (softmax over every position of image 2 of the scaled feature
+    correlation; flow = expected match - position), one convolutional
+    refinement; each flow upsampled x8 to full resolution, returned as
+    {'flow_preds': [matching, refined]} (adjusted_gmflow/gmflow/gmflow.py)."""
+
+    def __init__(self, dim: int = 64):
+        super().__init__()
+        self.enc = nn.Sequential(nn.Conv2d(3, 32, 7, 2, 3), nn.ReLU(inplace=True),
+                                 nn.Conv2d(32, 48, 3, 2, 1), nn.ReLU(inplace=True),
+                                 nn.Conv2d(48, dim, 3, 2, 1))
+        self.refine = nn.Sequential(nn.Conv2d(dim + 2, dim, 3, 1, 1), nn.ReLU(inplace=True),
+                                    nn.Conv2d(dim, 2, 3, 1, 1))
+
+    @staticmethod
+    def _up8(flow):
+        return F.interpolate(flow * 8, scale_factor=8, mode="bilinear", align_corners=True)
+
+    def forward(self, img1, img2, attn_splits_list=None, corr_radius_list=None, prop_radius_list=None):
+        x = torch.cat((img1, img2), 0) / 255.0
+        mean = x.new_tensor([0.485, 0.456, 0.406]).view(1, 3, 1, 1)  # gmflow/utils.py normalize_img
+        std = x.new_tensor([0.229, 0.224, 0.225]).view(1, 3, 1, 1)
+        f = self.enc((x - mean) / std)
+        f1, f2 = f.chunk(2, 0)
+        B, C, h, w = f1.shape
+        ys, xs = torch.meshgrid(torch.arange(h, device=f.device, dtype=f.dtype),
+                                torch.arange(w, device=f.device, dtype=f.dtype), indexing="ij")
+        grid = torch.stack((xs, ys), -1).view(1, h * w, 2)
+        corr = torch.bmm(f1.flatten(2).transpose(1, 2), f2.flatten(2)) / C ** 0.5  # [B, hw, hw]
+        match = torch.bmm(torch.softmax(corr, -1), grid.expand(B, -1, -1).to(corr.dtype))
+        flow = (match - grid).transpose(1, 2).reshape(B, 2, h, w)
+        preds = [self._up8(flow)]
+        flow = flow + self.refine(torch.cat((f1, flow.to(f1.dtype)), 1))
+        preds.append(self._up8(flow))
+        return {"flow_preds": preds}
+
+
+def fetch_gmflow_optimizer(model, lr=4e-4, weight_decay=1e-4, num_steps=100):
+    """adjusted_gmflow/main.py:230-231, :425-432: AdamW + cosine OneCycleLR."""
+    opt = torch.optim.AdamW(model.parameters(), lr=lr, weight_decay=weight_decay)
+    sched = torch.optim.lr_scheduler.OneCycleLR(opt, lr, num_steps + 10, pct_start=0.05, cycle_momentum=False,
+                                                anneal_strategy="cos")
+    return opt, sched
+
+
+def gmflow_train_step(model, optimizer, lr_scheduler, batch, device, args: StepArgs = StepArgs(gamma=0.9),
+                      ops: PairOps = PairOps(), dtype=torch.bfloat16, grad_clip=1.0,
+                      max_flow=GMFLOW_MAX_FLOW):
+    """One iteration of adjusted_gmflow/main.py:450-494 on a collated batch
+    of (rgb, raw depth, s, T, kind), the pair warped on the fly (make_pairs).
+    Returns (loss, metrics) as tensors, or None for a step the reference skips
+    (a NaN loss, :479-480: no update, no scheduler step -- the one host sync)."""
+    rgb, raw, s, T, kind = [x.to(device, non_blocking=True) for x in batch]
+    image1, image2, flow_gt, valid = make_pairs(rgb, raw, s, T, kind, ops, dtype)
+    dev_type = torch.device(device).type
+    with torch.autocast(dev_type, dtype=torch.bfloat16, enabled=args.amp):
+        results = model(image1.float(), image2.float(), attn_splits_list=[2], corr_radius_list=[-1],
+                        prop_radius_list=[-1])
+    loss, metrics = flow_loss_func(results["flow_preds"], flow_gt, valid, gamma=args.gamma, max_flow=max_flow)
+    if torch.isnan(loss):
+        return None
+    for p in model.parameters():  # :483-485
+        p.grad = None
+    loss.backward()
+    torch.nn.utils.clip_grad_norm_(model.parameters(), grad_clip)
+    optimizer.step()
+    if lr_scheduler is not None:
+        lr_scheduler.step()
+    return loss.detach(), {k: v.detach() for k, v in metrics.items()}
+
+
 # ---------------------------------------------------------------- driver
 def main(argv: Optional[Sequence[str]] = None):
     """torchrun entry: one process per GPU, DDP over RCCL (backend "nccl").
@@ -219,6 +320,8 @@ def main(argv: Optional[Sequence[str]] = None):
     ap.add_argument("--size", type=int, nargs=2, default=(368, 560))
     ap.add_argument("--iters", type=int, default=4)
     ap.add_argument("--workers", type=int, default=4)
+    ap.add_argument("--arch", choices=("raft", "gmflow"), default="raft",
+                    help="train step of adjusted_RAFT/train.py or adjusted_gmflow/main.py")
     a = ap.parse_args(argv)
     import torch.distributed as dist
     rank, world = int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
@@ -230,24 +333,32 @@ def main(argv: Optional[Sequence[str]] = None):
     if pg:
         dist.init_process_group("nccl", device_id=dev)
     torch.manual_seed(0)
-    model = IterativeFlowNet().to(dev)
+    gm = a.arch == "gmflow"
+    model = (GlobalMatchFlowNet() if gm else IterativeFlowNet()).to(dev)
     if pg:
         model = nn.parallel.DistributedDataParallel(model, device_ids=[local])
-    opt, sched = fetch_optimizer(model, num_steps=a.steps + a.warmup)
+    opt, sched = (fetch_gmflow_optimizer if gm else fetch_optimizer)(model, num_steps=a.steps + a.warmup)
     h, w = a.size
     total = a.steps + a.warmup
     loader = shard_loader(a.batch * world * total, h, w, a.batch, rank, world, workers=a.workers)
-    args = StepArgs(iters=a.iters)
+    args = StepArgs(iters=a.iters, gamma=0.9) if gm else StepArgs(iters=a.iters)
+
+    def step(b):
+        if gm:
+            r = gmflow_train_step(model, opt, sched, b, dev, args)
+            return r if r is not None else (torch.tensor(float("nan")), {"epe": torch.tensor(float("nan"))})
+        return train_step(model, opt, sched, b, dev, args)
+
     it = iter(loader)
     batches = [next(it) for _ in range(total)]  # host-side data ready: the step is what is timed
     for b in batches[:a.warmup]:
-        train_step(model, opt, sched, b, dev, args)
+        step(b)
     torch.cuda.synchronize()
     if pg:
         dist.barrier()
     t0 = time.perf_counter()
     for b in batches[a.warmup:]:
-        loss, m = train_step(model, opt, sched, b, dev, args)
+        loss, m = step(b)
     torch.cuda.synchronize()
     if pg:
         dist.barrier()
@@ -264,7 +375,8 @@ def main(argv: Optional[Sequence[str]] = None):
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     if rank == 0:
         pairs = a.steps * a.batch * world
-        print(json.dumps({"metric": "training pairs/s (on-the-fly bf16 warp + step)", "value": pairs / el.item(),
+        print(json.dumps({"metric": "training pairs/s (on-the-fly bf16 warp + step)", "arch": a.arch,
+                          "value": pairs / el.item(),
                           "n_gpus": world, "steps": a.steps, "ms_per_step": el.item() / a.steps * 1e3,
                           "pairs_ms_per_step": el_pairs / a.steps * 1e3,
                           "loss": float(loss), "epe": float(m["epe"]), "config": {"size": [h, w],

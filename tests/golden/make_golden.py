@@ -556,7 +556,48 @@ def make_ppa_fill_cases(utils_mod, ref_fw, Convert):
     return cases
 
 
+def make_loss_cases():
+    """The two training losses the on-the-fly step restates, run as the
+    reference has them: adjusted_RAFT/train.py's sequence_loss (taken by AST
+    with its MAX_FLOW; the module imports the RAFT network) and
+    adjusted_gmflow/loss.py's flow_loss_func (imported as is), on seeded
+    predictions, ground truth with some |flow| >= 400 and a ragged valid mask."""
+    src = open(os.path.join(REF, "adjusted_RAFT", "train.py")).read()
+    tree = ast.parse(src)
+    body = [n for n in tree.body if (isinstance(n, ast.Assign) and any(getattr(t, "id", "") == "MAX_FLOW"
+                                                                       for t in n.targets))
+            or (isinstance(n, ast.FunctionDef) and n.name == "sequence_loss")]
+    ns = {"torch": torch}
+    exec(compile(ast.Module(body=body, type_ignores=[]), os.path.join(REF, "adjusted_RAFT", "train.py"), "exec"), ns)
+    spec = importlib.util.spec_from_file_location("ref_gmflow_loss", os.path.join(REF, "adjusted_gmflow", "loss.py"))
+    gml = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(gml)
+    g = torch.Generator().manual_seed(7)
+    cases = {}
+    for n_pred, key in ((4, "raft"), (2, "gmflow")):
+        gt = torch.randn(2, 2, 12, 16, generator=g) * 60.0
+        gt[0, 0, :2, :3] = 450.0  # |flow| >= max_flow: excluded
+        preds = [gt + torch.randn(2, 2, 12, 16, generator=g) * (3.0 / (i + 1)) for i in range(n_pred)]
+        valid = (torch.rand(2, 12, 16, generator=g) > 0.2).float()
+        if key == "raft":
+            loss, m = ns["sequence_loss"](preds, gt, valid)
+        else:
+            loss, m = gml.flow_loss_func(preds, gt, valid)
+        cases[f"{key}/gt"] = gt.numpy()
+        cases[f"{key}/preds"] = torch.stack(preds).numpy()
+        cases[f"{key}/valid"] = valid.numpy()
+        cases[f"{key}/loss"] = np.float32(float(loss))
+        for k in ("epe", "1px", "3px", "5px"):
+            cases[f"{key}/{k}"] = np.float64(m[k])
+    return cases
+
+
 def main():
+    if sys.argv[1:] == ["losses"]:  # only the training-loss fixture
+        lc = make_loss_cases()
+        np.savez_compressed(os.path.join(HERE, "losses.npz"), **lc)
+        print("losses.npz", os.path.getsize(os.path.join(HERE, "losses.npz")), "bytes")
+        return
     ref_fw = load_reference_fw()
     geometry_mod = load_reference_geometry()
     utils_mod = load_reference_utils_subset()

@@ -1,6 +1,8 @@
 """On-the-fly bf16 warp inside a RAFT-style DDP train step (SURVEY.md 8(d)
 config 5, 8(f) rank 4; opticalflowfromdepth_amd/onthefly.py, following
-adjusted_RAFT/train.py:184-211).
+adjusted_RAFT/train.py:184-211) and a GMFlow-style one
+(adjusted_gmflow/main.py:450-494).  Both losses are pinned by the reference's
+own functions (tests/golden/losses.npz).
 
 CPU: the pair builder with the oracle's ops, and DDP over gloo at world size 2
 (two processes, each on its shard) against one process stepping the union of
@@ -112,6 +114,70 @@ def test_sequence_loss_follows_reference():
     assert torch.isclose(m["epe"], torch.tensor(2.0 * 2 ** 0.5))
 
 
+def _loss_fixture(key):
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "losses.npz"))
+    preds = [torch.from_numpy(p) for p in z[f"{key}/preds"]]
+    return preds, torch.from_numpy(z[f"{key}/gt"]), torch.from_numpy(z[f"{key}/valid"]), z
+
+
+@pytest.mark.parametrize("key", ["raft", "gmflow"])
+def test_losses_match_reference_fixture(key):
+    """sequence_loss (adjusted_RAFT/train.py:51-76) and flow_loss_func
+    (adjusted_gmflow/loss.py:4-37) against the reference's own functions run
+    on the same tensors (tests/golden/make_golden.py losses)."""
+    preds, gt, valid, z = _loss_fixture(key)
+    fn = otf.sequence_loss if key == "raft" else otf.flow_loss_func
+    loss, m = fn(preds, gt, valid)
+    assert float(loss) == pytest.approx(float(z[f"{key}/loss"]), rel=1e-6)
+    for k in ("epe", "1px", "3px", "5px"):
+        assert float(m[k]) == pytest.approx(float(z[f"{key}/{k}"]), rel=1e-6, abs=1e-12), k
+
+
+def _run_gm(steps, per_rank, device, ops, model_dim=16):
+    torch.manual_seed(0)
+    model = otf.GlobalMatchFlowNet(dim=model_dim).to(device)
+    opt, sched = otf.fetch_gmflow_optimizer(model, num_steps=steps)
+    args = otf.StepArgs(gamma=0.9, amp=False)
+    out = []
+    for b in _batches(0, 1, per_rank, steps):
+        r = otf.gmflow_train_step(model, opt, sched, b, device, args, ops)
+        out.append(r)
+    return model, opt, sched, out
+
+
+def test_gmflow_step_cpu_ops():
+    """adjusted_gmflow/main.py:450-494 on on-the-fly pairs: two predictions
+    per step (matching, refined), the OneCycle schedule advances once per
+    step, every parameter moves."""
+    torch.manual_seed(0)
+    init = otf.GlobalMatchFlowNet(dim=16).state_dict()
+    model, opt, sched, out = _run_gm(2, 2, "cpu", _cpu_ops())
+    assert all(r is not None and np.isfinite(float(r[0])) for r in out)
+    assert sched.last_epoch == 2
+    for k, v in model.state_dict().items():
+        assert not torch.equal(v, init[k]), k
+    b = _batches(0, 1, 2, 1)[0]
+    r = model(b[0], b[0])
+    assert set(r) == {"flow_preds"} and len(r["flow_preds"]) == 2 and r["flow_preds"][0].shape == (2, 2, H, W)
+
+
+def test_gmflow_step_skips_nan_loss():
+    """main.py:479-480: a NaN loss skips the step -- no update, no scheduler step."""
+    torch.manual_seed(0)
+    model = otf.GlobalMatchFlowNet(dim=16)
+    opt, sched = otf.fetch_gmflow_optimizer(model, num_steps=4)
+    before = {k: v.clone() for k, v in model.state_dict().items()}
+    nan_ops = otf.PairOps(warp=_cpu_ops().warp, ego_flow=lambda d, T: torch.full_like(d.expand(-1, 2, -1, -1),
+                                                                                       float("nan")),
+                          fill=_cpu_ops().fill)
+    b = _batches(0, 1, 2, 1)[0]
+    b[4][:] = 1  # ego-motion images only: every flow is NaN
+    r = otf.gmflow_train_step(model, opt, sched, b, "cpu", otf.StepArgs(gamma=0.9, amp=False), nan_ops)
+    assert r is None and sched.last_epoch == 0
+    for k, v in model.state_dict().items():
+        assert torch.equal(v, before[k]), k
+
+
 def test_ddp_gloo_world2_matches_single_process(tmp_path):
     per_rank, steps = 2, 2
     mp.spawn(_spawn_target, args=(2, per_rank, steps, str(tmp_path), 29731, "cpu"), nprocs=2, join=True)
@@ -162,6 +228,23 @@ def test_ddp_gloo_world2_on_gpu(tmp_path):
     for k in r0["params"]:
         assert torch.equal(r0["params"][k], r1["params"][k]), k
     assert all(np.isfinite(r0["losses"]))
+
+
+@pytest.mark.gpu
+def test_gmflow_step_on_gpu_loss_falls():
+    """The GMFlow-style step with the HIP pair builder at 368x560 under bf16
+    autocast, one batch repeated: finite and falling."""
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    model = otf.GlobalMatchFlowNet().to(dev)
+    opt, _ = otf.fetch_gmflow_optimizer(model, lr=1e-3)
+    b = next(iter(otf.shard_loader(2, 368, 560, 2, 0, 1)))
+    losses = []
+    for _ in range(30):
+        r = otf.gmflow_train_step(model, opt, None, b, dev, otf.StepArgs(gamma=0.9))
+        assert r is not None
+        losses.append(float(r[0]))
+    assert all(np.isfinite(losses)) and max(losses[-5:]) < losses[0], losses
 
 
 @pytest.mark.gpu
