@@ -225,6 +225,11 @@ __global__ __launch_bounds__(256) void sq_prep_kernel(const float *__restrict__ 
     const int x = blockIdx.x * 64 + (threadIdx.x & 63), y = blockIdx.y * 4 + (threadIdx.x >> 6);
     if (x >= W || y >= H) return;
     const int64_t HW = int64_t(H) * W, bl = blockIdx.z, b = b0 + bl;
+    if (x == 0) {  // the band counts sq_init_tile_kernel accumulates (padded rows y + 1, and 0, H + 1)
+        uint32_t *rc = w.rowc + bl * w.eh;
+        rc[y + 1] = 0u;
+        if (y == 0) rc[0] = rc[H + 1] = 0u;
+    }
     const float *v = valid + b * HW, *cl = coll + b * HW;
     const int64_t p = int64_t(y) * W + x;
     unsigned mp = 0;
@@ -290,6 +295,62 @@ __global__ __launch_bounds__(256) void sq_init_kernel(SqWs w, int range) {
         nband += __popcll(__ballot(band));
     }
     if (lane == 0) m.rowc[i] = nband;
+}
+
+// The same for range <= kInitR, on 64 x 16 tiles of the padded grid: the
+// tile's hole flags with a range-wide halo in LDS, the window test as a
+// horizontal then a vertical OR (separable), so a pixel costs ~2 (2r + 1)
+// LDS reads instead of (2r + 1)^2 global ones (the row kernel above read the
+// 7 x 7 window from memory for every pixel far from a hole: 1.6 ms per 64
+// images of 768 x 1024).  Band counts per row go to rowc by one atomic per
+// wave-row (PREP zeroed rowc).
+constexpr int kInitTW = 64, kInitTH = 16, kInitR = 8;
+__global__ __launch_bounds__(256) void sq_init_tile_kernel(SqWs w, int range) {
+    constexpr int XW = kInitTW + 2 * kInitR, YH = kInitTH + 2 * kInitR;
+    __shared__ uint8_t hf[YH][XW];        // hole flags, tile + halo
+    __shared__ uint8_t hor[YH][kInitTW];  // OR over [x - r, x + r] of each halo row
+    const Img m = image(w, blockIdx.z);
+    const int eh = m.eh, ew = m.ew, r = range;
+    const int i0 = int(blockIdx.y) * kInitTH, j0 = int(blockIdx.x) * kInitTW;
+    const int xw = kInitTW + 2 * r, yh = kInitTH + 2 * r;
+    for (int e = threadIdx.x; e < xw * yh; e += 256) {
+        const int ry = e / xw, rx = e - ry * xw;
+        const int y = i0 - r + ry, x = j0 - r + rx;
+        const bool h = y > 0 && x > 0 && y < eh - 1 && x < ew - 1 && m.sI[int64_t(y) * ew + x] == INF;
+        hf[ry][rx] = h ? 1 : 0;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < yh * kInitTW; e += 256) {
+        const int ry = e / kInitTW, cx = e - ry * kInitTW;
+        uint8_t o = 0;
+        for (int d = 0; d <= 2 * r; ++d) o |= hf[ry][cx + d];
+        hor[ry][cx] = o;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int j = j0 + lane;
+    for (int li = wave; li < kInitTH; li += 4) {
+        const int i = i0 + li;
+        if (i >= eh) break;  // wave-uniform
+        bool band = false;
+        if (j < ew) {
+            const int64_t p = int64_t(i) * ew + j;
+            const bool frame = i == 0 || j == 0 || i == eh - 1 || j == ew - 1;
+            const int hy = li + r, hx = lane + r;  // the pixel in hf
+            bool ring = false;
+            if (!frame && !hf[hy][hx]) {
+                band = hf[hy - 1][hx] || hf[hy + 1][hx] || hf[hy][hx - 1] || hf[hy][hx + 1];
+                if (!band)
+                    for (int d = 0; d <= 2 * r; ++d) ring = ring || hor[li + d][lane];
+            }
+            if (frame) m.sI[p] = 0u;
+            m.sO[p] = ring ? INF : 0u;
+            m.t[p] = band ? 0.f : T_FAR;
+            m.own[p] = INF;
+        }
+        const unsigned nb = unsigned(__popcll(__ballot(band)));
+        if (lane == 0 && nb) atomicAdd(&m.rowc[i], nb);
+    }
 }
 
 // Row offsets of the band (exclusive scan over rows), one workgroup per image.
@@ -1466,17 +1527,26 @@ __device__ __forceinline__ void val_pos(int e, int &a, int &b) {
 // that position (x in bits 0-1, y in bits 2-3); words 36-37 = dependants
 // mask over win_pos order; word 38 = cv2's weight sum).  Also the Kahn
 // counter (record index << 6 | earlier holes in the window) and level 0.
-__global__ __launch_bounds__(256) void sq_record3_kernel(SqWs w) {
-    // The workgroup's 64 x 4 pixels with a 4-pixel halo (clamped to the
+constexpr int kRecTH = 16;  // RECORD tile: 64 x kRecTH padded pixels per workgroup
+#ifndef OFD_REC_MINW  // RECORD waves per SIMD the register budget must allow (168 VGPRs at 3, no spill)
+#define OFD_REC_MINW 3
+#endif
+
+__global__ __launch_bounds__(256, OFD_REC_MINW) void sq_record3_kernel(SqWs w) {
+    // The workgroup's 64 x kRecTH pixels with a 4-pixel halo (clamped to the
     // padded image) of stamps and distances in LDS: every window read below
-    // is an LDS read.
-    constexpr int TR = 4 + 8, TC = 64 + 8;
+    // is an LDS read.  The tile's holes (~a fifth of its pixels) are listed
+    // first and dealt to the threads densely, so a wave's lanes all work
+    // (one thread per pixel left ~4 of 5 lanes idle in every wave).
+    constexpr int TR = kRecTH + 8, TC = 64 + 8;
     __shared__ uint32_t Ls[TR][TC];
     __shared__ float Lt[TR][TC];
-    const int j = blockIdx.x * 64 + (threadIdx.x & 63), i = blockIdx.y * 4 + (threadIdx.x >> 6);
-    const int i0 = int(blockIdx.y) * 4 - 4, j0 = int(blockIdx.x) * 64 - 4;
+    __shared__ uint16_t hl[64 * kRecTH];
+    __shared__ uint32_t nh;
+    const int i0 = int(blockIdx.y) * kRecTH - 4, j0 = int(blockIdx.x) * 64 - 4;
     const Img m = image(w, blockIdx.z);
     const int eh = m.eh, ew = m.ew;
+    if (threadIdx.x == 0) nh = 0u;
     for (int e = threadIdx.x; e < TR * TC; e += 256) {
         const int r = e / TC, c = e - r * TC;
         const int64_t q = int64_t(min(max(i0 + r, 0), eh - 1)) * ew + min(max(j0 + c, 0), ew - 1);
@@ -1484,84 +1554,98 @@ __global__ __launch_bounds__(256) void sq_record3_kernel(SqWs w) {
         Lt[r][c] = m.t[q];
     }
     __syncthreads();
-    if (i < 1 || j < 1 || i >= eh - 1 || j >= ew - 1) return;
-    const int64_t p = int64_t(i) * ew + j;
-    const int li = i - i0, lj = j - j0;
-    auto S = [&](int y, int x) -> uint32_t { return Ls[y - i0][x - j0]; };   // |y - i|, |x - j| <= 4
-    auto TT = [&](int y, int x) -> float { return Lt[y - i0][x - j0]; };
-    const uint32_t s = Ls[li][lj];
-    if (s == 0u || s == INF) return;
-    // records are indexed by padded pixel (the region holds en records), so
-    // COLOUR3 can address a dependant's record without a lookup
-    const uint32_t idx = uint32_t(p);
-    // Kahn counter and dependants: window positions inside the image (the
-    // tile's clamped halo holds the image's own pixels there)
-    uint32_t cnt = 0;
-    uint64_t dep = 0;
-    int bit = 0;
+    for (int e = threadIdx.x; e < 64 * kRecTH; e += 256) {
+        const int li = 4 + e / 64, lj = 4 + (e & 63);
+        const int i = i0 + li, j = j0 + lj;
+        const uint32_t sv = Ls[li][lj];
+        const bool hole = i >= 1 && j >= 1 && i < eh - 1 && j < ew - 1 && sv != 0u && sv != INF;
+        const uint64_t bal = __ballot(hole);
+        uint32_t base = 0;
+        if ((threadIdx.x & 63) == 0 && bal) base = atomicAdd(&nh, uint32_t(__popcll(bal)));
+        base = __shfl(base, 0);
+        if (hole) hl[base + __popcll(bal & ((uint64_t(1) << (threadIdx.x & 63)) - 1))] = uint16_t(e);
+    }
+    __syncthreads();
+    for (uint32_t h = threadIdx.x; h < nh; h += 256) {
+        const int e = hl[h];
+        const int li = 4 + e / 64, lj = 4 + (e & 63);
+        const int i = i0 + li, j = j0 + lj;
+        const int64_t p = int64_t(i) * ew + j;
+        auto S = [&](int y, int x) -> uint32_t { return Ls[y - i0][x - j0]; };   // |y - i|, |x - j| <= 4
+        auto TT = [&](int y, int x) -> float { return Lt[y - i0][x - j0]; };
+        const uint32_t s = Ls[li][lj];
+        // records are indexed by padded pixel (the region holds en records), so
+        // COLOUR3 can address a dependant's record without a lookup
+        const uint32_t idx = uint32_t(p);
+        // Kahn counter and dependants: window positions inside the image (the
+        // tile's clamped halo holds the image's own pixels there)
+        uint32_t cnt = 0;
+        uint64_t dep = 0;
+        int bit = 0;
 #pragma unroll
-    for (int a = -4; a <= 4; ++a)
+        for (int a = -4; a <= 4; ++a)
 #pragma unroll
-        for (int b = -4; b <= 4; ++b) {
-            if (!win3(a, b) || !(a || b)) continue;
-            const int y = i + a, x = j + b;
-            if (y >= 1 && x >= 1 && y < eh - 1 && x < ew - 1) {
-                const uint32_t q = S(y, x);
-                cnt += (q != 0u && q < s) ? 1u : 0u;
-                if (q > s && q != INF) dep |= uint64_t(1) << bit;
+            for (int b = -4; b <= 4; ++b) {
+                if (!win3(a, b) || !(a || b)) continue;
+                const int y = i + a, x = j + b;
+                if (y >= 1 && x >= 1 && y < eh - 1 && x < ew - 1) {
+                    const uint32_t q = S(y, x);
+                    cnt += (q != 0u && q < s) ? 1u : 0u;
+                    if (q > s && q != INF) dep |= uint64_t(1) << bit;
+                }
+                ++bit;
             }
-            ++bit;
-        }
-    // cv2's distance gradient at the hole
-    const uint32_t su = S(i - 1, j), sd = S(i + 1, j), sl = S(i, j - 1), sr = S(i, j + 1);
-    const float tij = TT(i, j), tu = TT(i - 1, j), td = TT(i + 1, j), tl = TT(i, j - 1), tr = TT(i, j + 1);
-    float gtx, gty;
-    if (!(sr >= s))
-        gtx = !(sl >= s) ? (tr - tl) * 0.5f : (tr - tij);
-    else
-        gtx = !(sl >= s) ? (tij - tl) : 0.f;
-    if (!(sd >= s))
-        gty = !(su >= s) ? (td - tu) * 0.5f : (td - tij);
-    else
-        gty = !(su >= s) ? (tij - tu) : 0.f;
-    uint32_t r[kRecW];
+        // cv2's distance gradient at the hole
+        const uint32_t su = S(i - 1, j), sd = S(i + 1, j), sl = S(i, j - 1), sr = S(i, j + 1);
+        const float tij = TT(i, j), tu = TT(i - 1, j), td = TT(i + 1, j), tl = TT(i, j - 1), tr = TT(i, j + 1);
+        float gtx, gty;
+        if (!(sr >= s))
+            gtx = !(sl >= s) ? (tr - tl) * 0.5f : (tr - tij);
+        else
+            gtx = !(sl >= s) ? (tij - tl) : 0.f;
+        if (!(sd >= s))
+            gty = !(su >= s) ? (td - tu) * 0.5f : (td - tij);
+        else
+            gty = !(su >= s) ? (tij - tu) : 0.f;
+        uint32_t r[kRecW];
 #pragma unroll
-    for (int k = 0; k < kRecW; ++k) r[k] = 0u;
-    float sum = 1.0e-20f;
-    int d = 0;
+        for (int k = 0; k < kRecW; ++k) r[k] = 0u;
+        float sum = 1.0e-20f;
+        int d = 0;
 #pragma unroll
-    for (int a = -3; a <= 3; ++a)
+        for (int a = -3; a <= 3; ++a)
 #pragma unroll
-        for (int b = -3; b <= 3; ++b) {
-            if (!disk3(a, b)) continue;
-            const int y = i + a, x = j + b;
-            const bool inimg = y > 0 && x > 0 && y < eh - 1 && x < ew - 1;
-            const bool used = inimg && !(S(y, x) >= s);
-            const float ry = float(-a), rx = float(-b);
-            const float len2 = rx * rx + ry * ry;
-            const float dst = float(1. / (double(len2) * sqrt(double(len2))));
-            const float lev = float(1. / (1 + fabs(double(TT(y, x) - tij))));
-            float dir = rx * gtx + ry * gty;
-            if (fabs(double(dir)) <= 0.01) dir = 0.000001f;
-            const float wt = used ? float(fabs(double(dst * lev * dir))) : 0.f;
-            sum += wt;
-            const bool nr = !(S(y, x + 1) >= s), nl = !(S(y, x - 1) >= s);
-            const bool nd = !(S(y + 1, x) >= s), nu = !(S(y - 1, x) >= s);
-            const uint32_t cx = nr ? (nl ? 0u : 1u) : (nl ? 2u : 3u);
-            const uint32_t cy = nd ? (nu ? 0u : 1u) : (nu ? 2u : 3u);
-            const int l = d % kL3, k = d / kL3;
-            r[4 * l + k] = __float_as_uint(wt);
-            r[32 + l / 2] |= (cx | (cy << 2)) << (16 * (l & 1) + 4 * k);
-            ++d;
-        }
-    r[36] = uint32_t(dep);
-    r[37] = uint32_t(dep >> 32);
-    r[38] = __float_as_uint(sum);
-    uint4 *dstp = reinterpret_cast<uint4 *>(m.rec + size_t(idx) * kRecW);
+            for (int b = -3; b <= 3; ++b) {
+                if (!disk3(a, b)) continue;
+                const int y = i + a, x = j + b;
+                const bool inimg = y > 0 && x > 0 && y < eh - 1 && x < ew - 1;
+                const bool used = inimg && !(S(y, x) >= s);
+                const float ry = float(-a), rx = float(-b);
+                const float len2 = rx * rx + ry * ry;
+                const float dst = float(1. / (double(len2) * sqrt(double(len2))));
+                const float lev = float(1. / (1 + fabs(double(TT(y, x) - tij))));
+                float dir = rx * gtx + ry * gty;
+                if (fabs(double(dir)) <= 0.01) dir = 0.000001f;
+                const float wt = used ? float(fabs(double(dst * lev * dir))) : 0.f;
+                sum += wt;
+                const bool nr = !(S(y, x + 1) >= s), nl = !(S(y, x - 1) >= s);
+                const bool nd = !(S(y + 1, x) >= s), nu = !(S(y - 1, x) >= s);
+                const uint32_t cx = nr ? (nl ? 0u : 1u) : (nl ? 2u : 3u);
+                const uint32_t cy = nd ? (nu ? 0u : 1u) : (nu ? 2u : 3u);
+                const int l = d % kL3, k = d / kL3;
+                r[4 * l + k] = __float_as_uint(wt);
+                r[32 + l / 2] |= (cx | (cy << 2)) << (16 * (l & 1) + 4 * k);
+                ++d;
+            }
+        r[36] = uint32_t(dep);
+        r[37] = uint32_t(dep >> 32);
+        r[38] = __float_as_uint(sum);
+        uint4 *dstp = reinterpret_cast<uint4 *>(m.rec + size_t(idx) * kRecW);
 #pragma unroll
-    for (int k = 0; k < kRecW / 4; ++k) dstp[k] = make_uint4(r[4 * k], r[4 * k + 1], r[4 * k + 2], r[4 * k + 3]);
-    m.own[p] = (idx << 6) | cnt;  // cnt <= 60; idx = p < en < 2^26 (the launcher's bound)
-    if (cnt == 0u) m.k0[atomicAdd(&m.meta[2], 1u)] = (uint64_t(idx) << 32) | uint64_t(p);
+        for (int k = 0; k < kRecW / 4; ++k) dstp[k] = make_uint4(r[4 * k], r[4 * k + 1], r[4 * k + 2], r[4 * k + 3]);
+        m.own[p] = (idx << 6) | cnt;  // cnt <= 60; idx = p < en < 2^26 (the launcher's bound)
+        if (cnt == 0u) m.k0[atomicAdd(&m.meta[2], 1u)] = (uint64_t(idx) << 32) | uint64_t(p);
+    }
 }
 
 struct C3Lds {
@@ -1861,7 +1945,13 @@ int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float 
         const int64_t nb = B - b0 < G ? B - b0 : G;
         hipLaunchKernelGGL(sq_prep_kernel, dim3(unsigned((W + 63) / 64), unsigned((H + 3) / 4), unsigned(nb)), dim3(256),
                            0, st, img, valid, collision, out, w, int(C), int(H), int(W), b0, rec3 ? 1 : 0);
-        hipLaunchKernelGGL(sq_init_kernel, dim3(unsigned((w.eh + 3) / 4), unsigned(nb)), dim3(256), 0, st, w, r);
+        if (r <= kInitR)
+            hipLaunchKernelGGL(sq_init_tile_kernel,
+                               dim3(unsigned((w.ew + kInitTW - 1) / kInitTW), unsigned((w.eh + kInitTH - 1) / kInitTH),
+                                    unsigned(nb)),
+                               dim3(256), 0, st, w, r);
+        else
+            hipLaunchKernelGGL(sq_init_kernel, dim3(unsigned((w.eh + 3) / 4), unsigned(nb)), dim3(256), 0, st, w, r);
         hipLaunchKernelGGL(sq_band_scan_kernel, dim3(unsigned(nb)), dim3(kThreads), 0, st, w);
         hipLaunchKernelGGL(sq_band_write_kernel, dim3(unsigned((w.eh + 3) / 4), unsigned(nb)), dim3(256), 0, st, w);
         hipLaunchKernelGGL(sq_fmm_kernel, dim3(unsigned(nb), 2u), dim3(kThreads), 0, st, w, bscale);
@@ -1869,7 +1959,8 @@ int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float 
         continue;  // probe: keep the record area (the inner march's bucket trace) for the host
 #endif
         if (rec3) {
-            hipLaunchKernelGGL(sq_record3_kernel, dim3(unsigned((w.ew + 63) / 64), unsigned((w.eh + 3) / 4), unsigned(nb)),
+            hipLaunchKernelGGL(sq_record3_kernel,
+                               dim3(unsigned((w.ew + 63) / 64), unsigned((w.eh + kRecTH - 1) / kRecTH), unsigned(nb)),
                                dim3(256), 0, st, w);
             hipLaunchKernelGGL(sq_colour3_kernel, dim3(unsigned(nb)), dim3(1024), 0, st, w, int(C), int(H), int(W));
             hipLaunchKernelGGL(sq_unpack_kernel, dim3(unsigned((H * W + 255) / 256), unsigned(nb)), dim3(256), 0, st, w,
