@@ -45,9 +45,9 @@ def main():
     key = (dev.index, torch.cuda.current_stream().cuda_stream)
     ws = ops._ip_workspaces[key]
     m = seq_meta(ws, B, 768, 1024)
-    print("meta columns: band, pushes, level0, levels, buckets, error")
+    print("meta columns: band, pushes, level0, levels, buckets, error, colour3 rounds, levels <= 64 holes")
     for k in np.argsort(-m[:, 3])[:8]:
-        print(k, m[k, :6].tolist())
+        print(k, m[k, :8].tolist())
     eh, ew = 770, 1026
     en = eh * ew
     pi_ = a256(en * 4) * 6 + a256(en * 8) * 2 + a256(eh * 4) + 32 * 4 + en * 160 + 768 * 1024 * 4 + en * 8 + 768
