@@ -169,13 +169,16 @@ class StepArgs:
 
 
 def train_step(model, optimizer, scheduler, batch, device, args: StepArgs, ops: PairOps = PairOps(),
-               dtype=torch.bfloat16):
+               dtype=torch.bfloat16, pair=None):
     """One iteration of adjusted_RAFT/train.py:185-211 on a collated batch of
-    (rgb, raw depth, s, T, kind); the pair is warped on the fly (make_pairs).
+    (rgb, raw depth, s, T, kind); the pair is warped on the fly (make_pairs),
+    or passed in ready (``pair``, e.g. from a PairPrefetcher).
     Returns the loss and metrics as tensors (no host sync)."""
     optimizer.zero_grad(set_to_none=True)
-    rgb, raw, s, T, kind = [x.to(device, non_blocking=True) for x in batch]
-    image1, image2, flow, valid = make_pairs(rgb, raw, s, T, kind, ops, dtype)
+    if pair is None:
+        rgb, raw, s, T, kind = [x.to(device, non_blocking=True) for x in batch]
+        pair = make_pairs(rgb, raw, s, T, kind, ops, dtype)
+    image1, image2, flow, valid = pair
     if args.add_noise:  # :188-191
         stdv = np.random.uniform(0.0, 5.0)
         image1 = (image1.float() + stdv * torch.randn(image1.shape, device=device)).clamp(0.0, 255.0)
@@ -283,13 +286,16 @@ def fetch_gmflow_optimizer(model, lr=4e-4, weight_decay=1e-4, num_steps=100):
 
 def gmflow_train_step(model, optimizer, lr_scheduler, batch, device, args: StepArgs = StepArgs(gamma=0.9),
                       ops: PairOps = PairOps(), dtype=torch.bfloat16, grad_clip=1.0,
-                      max_flow=GMFLOW_MAX_FLOW):
+                      max_flow=GMFLOW_MAX_FLOW, pair=None):
     """One iteration of adjusted_gmflow/main.py:450-494 on a collated batch
-    of (rgb, raw depth, s, T, kind), the pair warped on the fly (make_pairs).
+    of (rgb, raw depth, s, T, kind), the pair warped on the fly (make_pairs)
+    or passed in ready (``pair``).
     Returns (loss, metrics) as tensors, or None for a step the reference skips
     (a NaN loss, :479-480: no update, no scheduler step -- the one host sync)."""
-    rgb, raw, s, T, kind = [x.to(device, non_blocking=True) for x in batch]
-    image1, image2, flow_gt, valid = make_pairs(rgb, raw, s, T, kind, ops, dtype)
+    if pair is None:
+        rgb, raw, s, T, kind = [x.to(device, non_blocking=True) for x in batch]
+        pair = make_pairs(rgb, raw, s, T, kind, ops, dtype)
+    image1, image2, flow_gt, valid = pair
     dev_type = torch.device(device).type
     with torch.autocast(dev_type, dtype=torch.bfloat16, enabled=args.amp):
         results = model(image1.float(), image2.float(), attn_splits_list=[2], corr_radius_list=[-1],
@@ -307,6 +313,47 @@ def gmflow_train_step(model, optimizer, lr_scheduler, batch, device, args: StepA
     return loss.detach(), {k: v.detach() for k, v in metrics.items()}
 
 
+# ---------------------------------------------------------------- pair prefetch
+class PairPrefetcher:
+    """Builds step i+1's pair on a side stream while step i trains: the
+    cv2-order hole-fill holds one workgroup per image, so the network's
+    kernels run beside it on the rest of the chip.  ``get(batch)`` returns the
+    pair for ``batch`` (built earlier by ``put`` or now), with the caller's
+    stream ordered after it and the tensors marked as used there."""
+
+    def __init__(self, device, ops: PairOps = PairOps(), dtype=torch.bfloat16):
+        self.device, self.ops, self.dtype = torch.device(device), ops, dtype
+        self.side = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        self.pending = None
+
+    def _build(self, batch):
+        xs = [x.to(self.device, non_blocking=True) for x in batch]
+        return make_pairs(*xs, ops=self.ops, dtype=self.dtype)
+
+    def put(self, batch):
+        if self.side is None:
+            self.pending = (batch, self._build(batch), None)
+            return
+        self.side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self.side):
+            pair = self._build(batch)
+            ev = torch.cuda.Event()
+            ev.record(self.side)
+        self.pending = (batch, pair, ev)
+
+    def get(self, batch):
+        if self.pending is None or self.pending[0] is not batch:
+            self.put(batch)
+        _, pair, ev = self.pending
+        self.pending = None
+        if ev is not None:
+            cur = torch.cuda.current_stream(self.device)
+            cur.wait_event(ev)
+            for t in pair:
+                t.record_stream(cur)
+        return pair
+
+
 # ---------------------------------------------------------------- driver
 def main(argv: Optional[Sequence[str]] = None):
     """torchrun entry: one process per GPU, DDP over RCCL (backend "nccl").
@@ -322,6 +369,7 @@ def main(argv: Optional[Sequence[str]] = None):
     ap.add_argument("--workers", type=int, default=4)
     ap.add_argument("--arch", choices=("raft", "gmflow"), default="raft",
                     help="train step of adjusted_RAFT/train.py or adjusted_gmflow/main.py")
+    ap.add_argument("--no-prefetch", action="store_true", help="build each pair in the step (no side stream)")
     a = ap.parse_args(argv)
     import torch.distributed as dist
     rank, world = int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
@@ -343,22 +391,30 @@ def main(argv: Optional[Sequence[str]] = None):
     loader = shard_loader(a.batch * world * total, h, w, a.batch, rank, world, workers=a.workers)
     args = StepArgs(iters=a.iters, gamma=0.9) if gm else StepArgs(iters=a.iters)
 
-    def step(b):
+    pf = None if a.no_prefetch else PairPrefetcher(dev)
+
+    def step(b, nxt=None):
+        pair = None
+        if pf is not None:
+            pair = pf.get(b)
+            if nxt is not None:
+                pf.put(nxt)  # the next pair builds on the side stream during this step
         if gm:
-            r = gmflow_train_step(model, opt, sched, b, dev, args)
+            r = gmflow_train_step(model, opt, sched, b, dev, args, pair=pair)
             return r if r is not None else (torch.tensor(float("nan")), {"epe": torch.tensor(float("nan"))})
-        return train_step(model, opt, sched, b, dev, args)
+        return train_step(model, opt, sched, b, dev, args, pair=pair)
 
     it = iter(loader)
     batches = [next(it) for _ in range(total)]  # host-side data ready: the step is what is timed
-    for b in batches[:a.warmup]:
-        step(b)
+    for i, b in enumerate(batches[:a.warmup]):
+        step(b, batches[i + 1] if i + 1 < a.warmup else None)
     torch.cuda.synchronize()
     if pg:
         dist.barrier()
     t0 = time.perf_counter()
-    for b in batches[a.warmup:]:
-        loss, m = step(b)
+    timed = batches[a.warmup:]
+    for i, b in enumerate(timed):
+        loss, m = step(b, timed[i + 1] if i + 1 < len(timed) else None)
     torch.cuda.synchronize()
     if pg:
         dist.barrier()
@@ -376,6 +432,7 @@ def main(argv: Optional[Sequence[str]] = None):
     if rank == 0:
         pairs = a.steps * a.batch * world
         print(json.dumps({"metric": "training pairs/s (on-the-fly bf16 warp + step)", "arch": a.arch,
+                          "pair_prefetch": not a.no_prefetch,
                           "value": pairs / el.item(),
                           "n_gpus": world, "steps": a.steps, "ms_per_step": el.item() / a.steps * 1e3,
                           "pairs_ms_per_step": el_pairs / a.steps * 1e3,

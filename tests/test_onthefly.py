@@ -247,6 +247,35 @@ def test_gmflow_step_on_gpu_loss_falls():
     assert all(np.isfinite(losses)) and max(losses[-5:]) < losses[0], losses
 
 
+def test_prefetched_pair_equals_inline_pair_cpu():
+    """PairPrefetcher (no side stream on CPU) hands over the pair make_pairs builds."""
+    b = _batches(0, 1, 2, 1)[0]
+    pf = otf.PairPrefetcher("cpu", ops=_cpu_ops())
+    pf.put(b)
+    got = pf.get(b)
+    exp = otf.make_pairs(*b, ops=_cpu_ops())
+    assert all(torch.equal(x, y) for x, y in zip(got, exp))
+
+
+@pytest.mark.gpu
+def test_prefetched_pair_on_side_stream_equals_inline():
+    """The pair built on the side stream while another step runs is the same
+    pair, and the train step on it matches the step that builds its own."""
+    dev = torch.device("cuda:0")
+    bs = [next(iter(otf.shard_loader(2, 368, 560, 2, 0, 1, base=k))) for k in range(2)]
+    pf = otf.PairPrefetcher(dev)
+    pf.put(bs[0])
+    p0 = pf.get(bs[0])
+    pf.put(bs[1])
+    torch.cuda.synchronize()
+    e0 = otf.make_pairs(*[x.to(dev) for x in bs[0]])
+    p1 = pf.get(bs[1])
+    e1 = otf.make_pairs(*[x.to(dev) for x in bs[1]])
+    torch.cuda.synchronize()
+    for got, exp in ((p0, e0), (p1, e1)):
+        assert all(torch.equal(x, y) for x, y in zip(got, exp))
+
+
 @pytest.mark.gpu
 def test_train_step_loss_falls_on_a_fixed_batch():
     """bf16 autocast step at 368x560 (config 5 size) on one batch repeated: the loss falls."""
