@@ -373,6 +373,7 @@ class PreprocessPlusAugment(nn.Module):
         self.bf = BackFlow(device)
         self.inpaint_fn = inpaint_fn or inpaint
         self.writer = NpzWriter(writer_workers, compresslevel) if writer_workers > 0 else None
+        self.aug_streams = int(os.environ.get("OFD_PPA_STREAMS", "2"))
 
     # -- the first stage, batched: img0 [B,3,H,W], img0_depth [B,1,H,W] (raw), params per image
     def stage_one(self, img0, img0_depth, params: List[Dict]):
@@ -463,13 +464,47 @@ class PreprocessPlusAugment(nn.Module):
         return group44, groups
 
     def augment(self, groups, params: List[Dict], schedule: Sequence[int] = AUGMENT_SCHEDULE):
-        """Yields (group_idx, augment_idx, kind, data1 [B,8,H,W], data2 [B,8,H,W]) (preprocess.py:453-476)."""
-        for g, (imgA, dA, imgB, dB, fAB, bAB) in enumerate(groups):
-            for a, kind in enumerate(schedule):
-                set1, set2, _, _ = augment_flow_batch(imgA, dA, imgB, dB, fAB, bAB, kind,
-                                                      [p["augment"][g][a] for p in params], self.fw,
-                                                      inpaint_fn=self.inpaint_fn)
-                yield g, a, kind, torch.cat(set1[0:4], 1), torch.cat(set2[2:6], 1)
+        """Yields (group_idx, augment_idx, kind, data1 [B,8,H,W], data2 [B,8,H,W]) (preprocess.py:453-476).
+
+        The augmentations are independent of each other, and each one's
+        hole-fill (cv2's order: one workgroup per image, bound by the deepest
+        image's chain) leaves most of the chip idle, so on the GPU they run
+        round-robin on ``self.aug_streams`` side streams (OFD_PPA_STREAMS,
+        default 2; 0 = the caller's stream): consecutive augmentations' warps
+        and fills overlap.  Every yielded tensor is ready on the caller's
+        stream (it waits for the augmentation's event), and the caller's
+        stream waits for every side stream before the generator finishes."""
+        dev = groups[0][0].device
+        n_st = self.aug_streams if dev.type == "cuda" else 0
+        main = torch.cuda.current_stream(dev) if n_st else None
+        streams = [torch.cuda.Stream(dev) for _ in range(n_st)]
+        for st in streams:
+            st.wait_stream(main)  # the groups were made on the caller's stream
+        k = 0
+        try:
+            for g, (imgA, dA, imgB, dB, fAB, bAB) in enumerate(groups):
+                for a, kind in enumerate(schedule):
+                    ps = [p["augment"][g][a] for p in params]
+                    if not streams:
+                        set1, set2, _, _ = augment_flow_batch(imgA, dA, imgB, dB, fAB, bAB, kind, ps, self.fw,
+                                                              inpaint_fn=self.inpaint_fn)
+                        yield g, a, kind, torch.cat(set1[0:4], 1), torch.cat(set2[2:6], 1)
+                        continue
+                    st = streams[k % len(streams)]
+                    k += 1
+                    with torch.cuda.stream(st):
+                        set1, set2, _, _ = augment_flow_batch(imgA, dA, imgB, dB, fAB, bAB, kind, ps, self.fw,
+                                                              inpaint_fn=self.inpaint_fn)
+                        d1, d2 = torch.cat(set1[0:4], 1), torch.cat(set2[2:6], 1)
+                        ev = torch.cuda.Event()
+                        ev.record(st)
+                    main.wait_event(ev)
+                    d1.record_stream(main)
+                    d2.record_stream(main)
+                    yield g, a, kind, d1, d2
+        finally:
+            for st in streams:
+                main.wait_stream(st)
 
     def run_batch(self, seeds: Sequence[int], img0, img0_depth, is_stereo=False, out_dirs=None,
                   schedule: Sequence[int] = AUGMENT_SCHEDULE, augment=True):
