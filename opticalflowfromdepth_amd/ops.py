@@ -43,7 +43,9 @@ _F32, _F64, _BF16 = torch.float32, torch.float64, torch.bfloat16
 # stream, so the caching allocator hands its memory out again only in that
 # stream's order.
 _ws_lock = threading.Lock()
-_WS_CACHE_MAX = 4
+# (8: the pipeline's caller stream and three augmentation streams, plus a
+# few more, keep their workspaces; OFD_WS_CACHE_MAX overrides)
+_WS_CACHE_MAX = int(os.environ.get("OFD_WS_CACHE_MAX", "8"))
 _workspaces: "OrderedDict[Tuple[int, int], torch.Tensor]" = OrderedDict()
 # hole-fill scratch, one per (device, stream); needs no initialisation
 _ip_workspaces: "OrderedDict[Tuple[int, int], torch.Tensor]" = OrderedDict()

@@ -373,7 +373,11 @@ class PreprocessPlusAugment(nn.Module):
         self.bf = BackFlow(device)
         self.inpaint_fn = inpaint_fn or inpaint
         self.writer = NpzWriter(writer_workers, compresslevel) if writer_workers > 0 else None
-        self.aug_streams = int(os.environ.get("OFD_PPA_STREAMS", "2"))
+        # side streams for the augmentations: with the caller's stream, 4 =
+        # the HIP runtime's hardware queues per process (GPU_MAX_HW_QUEUES);
+        # more share queues and serialise (profiles/r03_pipeline_streams.txt)
+        self.aug_streams = int(os.environ.get("OFD_PPA_STREAMS", "3"))
+        self._streams = None
 
     # -- the first stage, batched: img0 [B,3,H,W], img0_depth [B,1,H,W] (raw), params per image
     def stage_one(self, img0, img0_depth, params: List[Dict]):
@@ -470,14 +474,18 @@ class PreprocessPlusAugment(nn.Module):
         hole-fill (cv2's order: one workgroup per image, bound by the deepest
         image's chain) leaves most of the chip idle, so on the GPU they run
         round-robin on ``self.aug_streams`` side streams (OFD_PPA_STREAMS,
-        default 2; 0 = the caller's stream): consecutive augmentations' warps
+        default 3; 0 = the caller's stream): consecutive augmentations' warps
         and fills overlap.  Every yielded tensor is ready on the caller's
         stream (it waits for the augmentation's event), and the caller's
         stream waits for every side stream before the generator finishes."""
         dev = groups[0][0].device
         n_st = self.aug_streams if dev.type == "cuda" else 0
         main = torch.cuda.current_stream(dev) if n_st else None
-        streams = [torch.cuda.Stream(dev) for _ in range(n_st)]
+        # created once per instance: each stream keeps its warp and hole-fill
+        # workspaces (ops' per-stream caches) across batches
+        if n_st and (self._streams is None or self._streams[0].device != dev):
+            self._streams = [torch.cuda.Stream(dev) for _ in range(n_st)]
+        streams = self._streams if n_st else []
         for st in streams:
             st.wait_stream(main)  # the groups were made on the caller's stream
         k = 0
