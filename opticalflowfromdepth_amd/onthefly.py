@@ -315,37 +315,43 @@ def gmflow_train_step(model, optimizer, lr_scheduler, batch, device, args: StepA
 
 # ---------------------------------------------------------------- pair prefetch
 class PairPrefetcher:
-    """Builds step i+1's pair on a side stream while step i trains: the
-    cv2-order hole-fill holds one workgroup per image, so the network's
-    kernels run beside it on the rest of the chip.  ``get(batch)`` returns the
-    pair for ``batch`` (built earlier by ``put`` or now), with the caller's
-    stream ordered after it and the tensors marked as used there."""
+    """Builds the next steps' pairs on side streams while the current step
+    trains: the cv2-order hole-fill holds one workgroup per image (its time
+    is the deepest image's chain), so the network's kernels and other pairs'
+    fills run beside it on the rest of the chip.  ``put(batch)`` starts a
+    pair (round-robin over ``streams`` side streams); ``get(batch)`` returns
+    the pair for ``batch`` (built earlier by ``put`` or now), with the
+    caller's stream ordered after it and its tensors marked as used there."""
 
-    def __init__(self, device, ops: PairOps = PairOps(), dtype=torch.bfloat16):
+    def __init__(self, device, ops: PairOps = PairOps(), dtype=torch.bfloat16, streams: int = 2):
         self.device, self.ops, self.dtype = torch.device(device), ops, dtype
-        self.side = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
-        self.pending = None
+        self.sides = [torch.cuda.Stream(self.device) for _ in range(streams)] if self.device.type == "cuda" else []
+        self.pending = {}  # id(batch) -> (batch, pair, event)
+        self.k = 0
 
     def _build(self, batch):
         xs = [x.to(self.device, non_blocking=True) for x in batch]
         return make_pairs(*xs, ops=self.ops, dtype=self.dtype)
 
     def put(self, batch):
-        if self.side is None:
-            self.pending = (batch, self._build(batch), None)
+        if id(batch) in self.pending:
             return
-        self.side.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(self.side):
+        if not self.sides:
+            self.pending[id(batch)] = (batch, self._build(batch), None)
+            return
+        side = self.sides[self.k % len(self.sides)]
+        self.k += 1
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):
             pair = self._build(batch)
             ev = torch.cuda.Event()
-            ev.record(self.side)
-        self.pending = (batch, pair, ev)
+            ev.record(side)
+        self.pending[id(batch)] = (batch, pair, ev)
 
     def get(self, batch):
-        if self.pending is None or self.pending[0] is not batch:
+        if id(batch) not in self.pending:
             self.put(batch)
-        _, pair, ev = self.pending
-        self.pending = None
+        _, pair, ev = self.pending.pop(id(batch))
         if ev is not None:
             cur = torch.cuda.current_stream(self.device)
             cur.wait_event(ev)
@@ -393,12 +399,12 @@ def main(argv: Optional[Sequence[str]] = None):
 
     pf = None if a.no_prefetch else PairPrefetcher(dev)
 
-    def step(b, nxt=None):
+    def step(b, nxt=()):
         pair = None
         if pf is not None:
+            for n in nxt:
+                pf.put(n)  # the next steps' pairs build on the side streams during this step
             pair = pf.get(b)
-            if nxt is not None:
-                pf.put(nxt)  # the next pair builds on the side stream during this step
         if gm:
             r = gmflow_train_step(model, opt, sched, b, dev, args, pair=pair)
             return r if r is not None else (torch.tensor(float("nan")), {"epe": torch.tensor(float("nan"))})
@@ -406,15 +412,17 @@ def main(argv: Optional[Sequence[str]] = None):
 
     it = iter(loader)
     batches = [next(it) for _ in range(total)]  # host-side data ready: the step is what is timed
-    for i, b in enumerate(batches[:a.warmup]):
-        step(b, batches[i + 1] if i + 1 < a.warmup else None)
+    ahead = 2  # pairs in flight beside the current step (one per side stream)
+    warm = batches[:a.warmup]
+    for i, b in enumerate(warm):
+        step(b, warm[i + 1:i + 1 + ahead])
     torch.cuda.synchronize()
     if pg:
         dist.barrier()
     t0 = time.perf_counter()
     timed = batches[a.warmup:]
     for i, b in enumerate(timed):
-        loss, m = step(b, timed[i + 1] if i + 1 < len(timed) else None)
+        loss, m = step(b, timed[i + 1:i + 1 + ahead])
     torch.cuda.synchronize()
     if pg:
         dist.barrier()
