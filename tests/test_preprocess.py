@@ -363,3 +363,31 @@ def test_run_batch_with_the_default_fill_matches_reference(tmp_path, workers):
     ppa.run_batch(seeds, img0, raw, out_dirs=dirs)
     for n in range(2):
         _check_dir_vs_fill_fixture(z, n, dirs[n])
+
+
+@pytest.mark.gpu
+def test_augment_streams_give_the_same_batch_as_one_stream():
+    """The augmentations round-robin on side streams (augment(), 3 by default)
+    produce exactly the tensors the caller's stream alone produces, at a size
+    where every augmentation's warps and fills overlap (4 images of 96x128:
+    disparity and ego-motion groups, every augment kind)."""
+    from opticalflowfromdepth_amd import preprocess as pp, synth
+    dev = torch.device("cuda:0")
+    seeds = [101, 202, 303, 404]
+    img0 = synth.synthetic_rgb(seeds, 96, 128, dev)
+    depth = synth.synthetic_depth(seeds, 96, 128, dev, dtype=torch.float64)
+    runs = []
+    for n_st in (0, 3):
+        ppa = pp.PreprocessPlusAugment(dev)
+        ppa.aug_streams = n_st
+        params = [pp.draw_image_params(s, 96, 128) for s in seeds]
+        group44, groups = ppa.stage_one(img0, depth, params)
+        outs = [(g, a, k, d1.clone(), d2.clone()) for g, a, k, d1, d2 in ppa.augment(groups, params)]
+        torch.cuda.synchronize()
+        runs.append((group44, outs))
+    (g0, o0), (g1, o1) = runs
+    assert torch.equal(g0, g1)
+    assert len(o0) == len(o1) == 60
+    for (ga, aa, ka, d1a, d2a), (gb, ab, kb, d1b, d2b) in zip(o0, o1):
+        assert (ga, aa, ka) == (gb, ab, kb)
+        assert torch.equal(d1a, d1b) and torch.equal(d2a, d2b), (ga, aa, ka)
