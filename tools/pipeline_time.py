@@ -36,7 +36,11 @@ if args.ip_schedule:
 seeds = [12345 + i for i in range(B)]
 img0 = synth.synthetic_rgb(seeds, H, W, dev)
 depth = synth.synthetic_depth(seeds, H, W, dev, dtype=torch.float64)
-pp.PreprocessPlusAugment(dev).run_batch(seeds[:2], img0[:2], depth[:2], augment=False)  # warm-up
+# warm-up: one full batch, so the timed call finds every stream's warp and
+# hole-fill workspaces allocated (the steady state of a run over many batches)
+_warm = pp.PreprocessPlusAugment(dev)
+_warm.run_batch(seeds, img0, depth, augment=not args.no_augment)
+torch.cuda.synchronize()
 root = args.dir or tempfile.gettempdir()
 for mode in args.save:
     workers, level = 0, 6
@@ -44,6 +48,7 @@ for mode in args.save:
         n, level = mode[4:].split(":")
         workers, level = int(n), int(level)
     ppa = pp.PreprocessPlusAugment(dev, writer_workers=workers, compresslevel=level)
+    ppa._streams = _warm._streams  # the warmed streams (their workspaces are cached per stream)
     if mode.startswith("gpu"):
         from opticalflowfromdepth_amd.npz_gpu import GpuNpzWriter
         ppa.writer = GpuNpzWriter(workers=int(mode[3:] or 8))
