@@ -51,10 +51,18 @@ _workspaces: "OrderedDict[Tuple[int, int], torch.Tensor]" = OrderedDict()
 _ip_workspaces: "OrderedDict[Tuple[int, int], torch.Tensor]" = OrderedDict()
 
 
+# bytes all cached workspaces of one kind may hold together (the hole-fill's
+# reach ~21 GB per stream at 128 images of 768x1024): least recently used
+# entries beyond it are dropped, the newest one always stays
+_WS_CACHE_BYTES = int(float(os.environ.get("OFD_WS_CACHE_GB", "128")) * (1 << 30))
+
+
 def _cache_put(cache: OrderedDict, key, ws: torch.Tensor) -> None:
     cache[key] = ws
     cache.move_to_end(key)
     while len(cache) > _WS_CACHE_MAX:
+        cache.popitem(last=False)
+    while len(cache) > 1 and sum(t.numel() for t in cache.values()) > _WS_CACHE_BYTES:
         cache.popitem(last=False)
 
 

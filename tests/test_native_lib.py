@@ -180,3 +180,19 @@ def test_c_abi_header_compiles_as_c():
                            '(void)f; (void)g; return OFD_FW_OK;}\n')
         subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-c", "-I", os.path.join(REPO, "include"),
                         c, "-o", os.path.join(d, "t.o")], check=True)
+
+
+def test_workspace_cache_bounds_count_and_bytes(monkeypatch):
+    """ops' per-stream workspace caches drop least-recently-used entries past
+    their count and byte bounds, and always keep the newest."""
+    from collections import OrderedDict
+    import torch
+    from opticalflowfromdepth_amd import ops
+    monkeypatch.setattr(ops, "_WS_CACHE_MAX", 3)
+    monkeypatch.setattr(ops, "_WS_CACHE_BYTES", 250)
+    c = OrderedDict()
+    for k in range(4):
+        ops._cache_put(c, k, torch.empty(100, dtype=torch.uint8))
+    assert list(c) == [2, 3]  # 4 entries > 3, then 300 bytes > 250
+    ops._cache_put(c, 9, torch.empty(1000, dtype=torch.uint8))
+    assert list(c) == [9]  # alone over the byte bound: kept
