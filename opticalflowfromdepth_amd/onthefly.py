@@ -397,7 +397,8 @@ def main(argv: Optional[Sequence[str]] = None):
     loader = shard_loader(a.batch * world * total, h, w, a.batch, rank, world, workers=a.workers)
     args = StepArgs(iters=a.iters, gamma=0.9) if gm else StepArgs(iters=a.iters)
 
-    pf = None if a.no_prefetch else PairPrefetcher(dev)
+    ahead = int(os.environ.get("OFD_PAIRS_AHEAD", "2"))  # pairs in flight beside the current step
+    pf = None if a.no_prefetch else PairPrefetcher(dev, streams=max(ahead, 1))
 
     def step(b, nxt=()):
         pair = None
@@ -412,7 +413,6 @@ def main(argv: Optional[Sequence[str]] = None):
 
     it = iter(loader)
     batches = [next(it) for _ in range(total)]  # host-side data ready: the step is what is timed
-    ahead = 2  # pairs in flight beside the current step (one per side stream)
     warm = batches[:a.warmup]
     for i, b in enumerate(warm):
         step(b, warm[i + 1:i + 1 + ahead])
