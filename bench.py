@@ -711,6 +711,7 @@ def main(argv=None):
             "fused_ego": fused_ego,
             "bf16_warp": bf16,
             "ranks": ranks,
+            "build_id": _native.build_id(),
         }
         print(json.dumps(rec), flush=True)
     finish(world)

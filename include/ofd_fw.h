@@ -74,6 +74,13 @@ enum {
 /* ABI version of the loaded library (OFD_FW_ABI_VERSION at build time). */
 int ofd_fw_abi_version(void);
 
+/* Build id of the loaded library: the first 16 hex digits of the SHA-256 of
+ * the sources it was compiled from (the .hip files and ip_common.h under csrc,
+ * the headers under include;
+ * opticalflowfromdepth_amd/build.py:source_hash), or "unknown" for a build
+ * made without it.  Ties a binary to the commit whose sources it came from. */
+const char *ofd_fw_build_id(void);
+
 /* Engines (see csrc/ofd_fw.hip): TILE = LDS z-buffer per target tile whose
  * workgroup also gathers the output (default); TILE_SPLIT = the same z-buffer
  * publishing a winner map, then a separate RESOLVE gather pass; ATOMIC = one

@@ -30,6 +30,7 @@ _I64 = ctypes.c_int64
 _SZ = ctypes.c_size_t
 SIGNATURES = {
     "ofd_fw_abi_version": ([], ctypes.c_int),
+    "ofd_fw_build_id": ([], ctypes.c_char_p),
     "ofd_fw_strerror": ([ctypes.c_int], ctypes.c_char_p),
     "ofd_fw_set_engine": ([ctypes.c_int], ctypes.c_int),
     "ofd_fw_set_disparity_rows": ([ctypes.c_int], ctypes.c_int),
@@ -73,19 +74,26 @@ def _try_build():
 
 
 def lib():
-    """Return the loaded ctypes library, building it once if it is absent."""
+    """Return the loaded ctypes library.  The in-tree library is (re)built
+    first unless it was built from the current sources (build.needs_build: a
+    content hash, recorded beside the .so), and after loading, the id the
+    binary itself carries (ofd_fw_build_id) must equal that hash -- a stale
+    .so that travelled with a tree can never stand in for the sources under
+    test.  OFD_FW_LIB (probe builds) skips both checks."""
     global _lib
     if _lib is not None:
         return _lib
     with _lock:
         if _lib is not None:
             return _lib
-        if not os.path.exists(LIB_PATH):
+        override = bool(os.environ.get("OFD_FW_LIB"))
+        from . import build as _build
+        if not override and (not os.path.exists(LIB_PATH) or _build.needs_build()):
             try:
                 _try_build()
             except Exception as e:  # pragma: no cover - depends on toolchain
                 raise NativeLibraryError(
-                    f"libofd_fw.so not found at {LIB_PATH} and building it failed: {e}") from e
+                    f"libofd_fw.so at {LIB_PATH} is missing or stale and building it failed: {e}") from e
         try:
             l = ctypes.CDLL(LIB_PATH)
         except OSError as e:
@@ -97,8 +105,18 @@ def lib():
         v = l.ofd_fw_abi_version()
         if v != ABI_VERSION:
             raise NativeLibraryError(f"libofd_fw ABI {v}, python expects {ABI_VERSION}; rebuild")
+        if not override:
+            got, want = l.ofd_fw_build_id().decode(), _build.source_hash()
+            if got != want:
+                raise NativeLibraryError(f"{LIB_PATH} carries build id {got}, the sources hash to {want}; "
+                                         "rebuild (python -m opticalflowfromdepth_amd.build)")
         _lib = l
         return _lib
+
+
+def build_id() -> str:
+    """The loaded library's build id (include/ofd_fw.h: ofd_fw_build_id)."""
+    return lib().ofd_fw_build_id().decode()
 
 
 def check(rc: int, what: str) -> None:

@@ -32,11 +32,37 @@ def hipcc() -> str:
     raise FileNotFoundError("hipcc not found (set HIPCC or install ROCm)")
 
 
+ID_FILE = OUT + ".id"
+
+
+def source_hash() -> str:
+    """The build id: first 16 hex digits of the SHA-256 over every source
+    the library is compiled from (name and bytes, in a fixed order).  The
+    library embeds it (ofd_fw_build_id) and a sidecar file records it, so a
+    binary can be tied to the sources -- i.e. the commit -- it came from."""
+    import hashlib
+    h = hashlib.sha256()
+    for p in SRCS + HDRS:
+        h.update(os.path.relpath(p, REPO).encode() + b"\0")
+        with open(p, "rb") as f:
+            h.update(f.read())
+        h.update(b"\0")
+    return h.hexdigest()[:16]
+
+
+def built_id() -> str | None:
+    """The build id the in-tree library was built with (its sidecar), or None."""
+    try:
+        with open(ID_FILE) as f:
+            return f.read().strip() or None
+    except OSError:
+        return None
+
+
 def needs_build() -> bool:
-    if not os.path.exists(OUT):
-        return True
-    t = os.path.getmtime(OUT)
-    return any(os.path.getmtime(p) > t for p in SRCS + HDRS + [os.path.abspath(__file__)])
+    """True unless the in-tree library exists and was built from the current
+    sources (content hash, not mtimes: a copied tree keeps its verdict)."""
+    return not os.path.exists(OUT) or built_id() != source_hash()
 
 
 def build_native(force: bool = False, verbose: bool = False) -> str:
@@ -46,12 +72,16 @@ def build_native(force: bool = False, verbose: bool = False) -> str:
     tmp = OUT + f".tmp{os.getpid()}"
     # -ffp-contract=off: the hole-fill's float / double sequence must be the
     # oracle's bit for bit (the warp has no contractible arithmetic)
+    bid = source_hash()
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
-           "-Wall", "-I", os.path.join(REPO, "include"), "-o", tmp] + SRCS
+           "-Wall", f'-DOFD_BUILD_ID="{bid}"', "-I", os.path.join(REPO, "include"), "-o", tmp] + SRCS
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
     os.replace(tmp, OUT)  # atomic: concurrent builders never expose a half-written .so
+    with open(ID_FILE + f".tmp{os.getpid()}", "w") as f:
+        f.write(bid + "\n")
+    os.replace(ID_FILE + f".tmp{os.getpid()}", ID_FILE)
     build_c_host()
     return OUT
 

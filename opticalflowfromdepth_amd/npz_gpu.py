@@ -135,11 +135,19 @@ class GpuNpzWriter:
     """Drop-in for NpzWriter (preprocess.py's product files) with the arrays
     deflated on the GPU.  ``save_batch(paths, x, key, extra)`` writes one npz
     per leading index of the device tensor x (one ofd_deflate_batch call for
-    all of them); the compressed streams come to pinned host memory behind an
-    event, and a small thread pool assembles and writes the zips."""
+    all of them) and returns without waiting for the GPU: the stream sizes
+    and CRCs go to pinned host memory behind an event; a pool thread waits
+    for that event, copies the compressed streams to pinned memory on a side
+    stream, and hands the zips to the other pool threads.  The caller's
+    stream therefore keeps its queue full (augmentations already queued on
+    it, or on side streams, keep running while earlier files deflate)."""
 
     def __init__(self, workers: int = 8, header_level: int = 6, max_pending_bytes: int = 8 << 30):
         self.pool = ThreadPoolExecutor(max_workers=workers, thread_name_prefix="gnpz")
+        # one fetch thread: waits for each batch's deflate, then for room under
+        # max_pending_bytes, then copies the streams; it never occupies a
+        # writer thread, so the writes that free room always make progress
+        self.fetcher = ThreadPoolExecutor(max_workers=1, thread_name_prefix="gnpz-fetch")
         self.level = header_level
         self.cap = max_pending_bytes
         self.pending = 0
@@ -147,14 +155,27 @@ class GpuNpzWriter:
         self.futures = []
         self.bytes_written = 0       # compressed bytes on disk
         self.bytes_in = 0            # array bytes deflated
-        self._ws = {}
+        self._ws = {}                # (device, stream) -> deflate workspace
+        self._copy_streams = {}      # device -> side stream of the D2H copies
+        self._lock = threading.Lock()
 
-    def _workspace(self, dev, nbytes):
-        ws = self._ws.get(dev)
-        if ws is None or ws.numel() < nbytes:
-            ws = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=dev)
-            self._ws[dev] = ws
-        return ws
+    def _workspace(self, dev, stream, nbytes):
+        # keyed by (device, stream): two deflates in flight on different
+        # streams never share scratch; calls on one stream are ordered by it
+        k = (dev, stream.cuda_stream)
+        with self._lock:
+            ws = self._ws.get(k)
+            if ws is None or ws.numel() < nbytes:
+                ws = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=dev)
+                self._ws[k] = ws
+            return ws
+
+    def _copy_stream(self, dev):
+        with self._lock:
+            s = self._copy_streams.get(dev)
+            if s is None:
+                s = self._copy_streams[dev] = torch.cuda.Stream(dev)
+            return s
 
     def save_batch(self, paths: Sequence[str], x: torch.Tensor, key: str = "img_depth_flow",
                    extra: Optional[Dict[str, object]] = None) -> None:
@@ -164,8 +185,10 @@ class GpuNpzWriter:
         count = x.shape[0]
         if len(paths) != count:
             raise ValueError(f"{len(paths)} paths for {count} arrays")
+        if count == 0:
+            return
         lib = _native.lib()
-        each = int(x[0].numel() * x.element_size()) if count else 0
+        each = int(x[0].numel() * x.element_size())
         bound = int(lib.ofd_deflate_bound(each))
         dev = x.device
         with torch.cuda.device(dev):
@@ -174,32 +197,25 @@ class GpuNpzWriter:
             sizes = torch.empty(count, dtype=torch.int64, device=dev)
             crcs = torch.empty(count, dtype=torch.int32, device=dev)
             nws = int(lib.ofd_deflate_workspace_bytes(count, each))
-            ws = self._workspace(dev, nws) if nws else None
+            ws = self._workspace(dev, stream, nws) if nws else None
             rc = lib.ofd_deflate_batch(x.data_ptr(), count, each, out.data_ptr(), sizes.data_ptr(), crcs.data_ptr(),
                                        ws.data_ptr() if ws is not None else None, nws, stream.cuda_stream)
             _native.check(rc, "ofd_deflate_batch")
-            sz = sizes.cpu().tolist()                   # small: waits for the deflate only
-            cr = [c & 0xFFFFFFFF for c in crcs.cpu().tolist()]
-            total = sum(sz)
-            with self.cv:
-                while self.pending > 0 and self.pending + total > self.cap:
-                    self.cv.wait()
-                self.pending += total
-            host = torch.empty(total, dtype=torch.uint8, pin_memory=True)
-            o = 0
-            for i, n in enumerate(sz):               # the streams, back to back, one D2H each
-                host[o:o + n].copy_(out[i * bound:i * bound + n], non_blocking=True)
-                o += n
-            ev = torch.cuda.Event()
-            ev.record(stream)
+            sz_h = torch.empty(count, dtype=torch.int64, pin_memory=True)
+            cr_h = torch.empty(count, dtype=torch.int32, pin_memory=True)
+            sz_h.copy_(sizes, non_blocking=True)
+            cr_h.copy_(crcs, non_blocking=True)
+            ev_sizes = torch.cuda.Event()
+            ev_sizes.record(stream)
+            side = self._copy_stream(dev)
+            out.record_stream(side)  # the D2H copies below read it on the side stream
         shape, dtype = tuple(x.shape[1:]), np.dtype(str(x.dtype).replace("torch.", ""))
         extra = dict(extra or {})
         self.bytes_in += each * count
 
-        def job(i, off, n):
-            ev.synchronize()
+        def write_one(host, i, off, n, crc):
             mv = memoryview(host.numpy())[off:off + n]
-            mem = [member_from_gpu_stream(key, shape, dtype, mv, cr[i], each, self.level)]
+            mem = [member_from_gpu_stream(key, shape, dtype, mv, crc, each, self.level)]
             mem += [member_from_array(k, v, self.level) for k, v in extra.items()]
             return write_zip(paths[i], mem)
 
@@ -210,12 +226,37 @@ class GpuNpzWriter:
                     self.bytes_written += f.result()
                 self.cv.notify_all()
 
-        o = 0
-        for i, n in enumerate(sz):
-            fut = self.pool.submit(job, i, o, n)
-            fut.add_done_callback(lambda f, n=n: done(f, n))
+        def fetch():
+            # runs on the fetch thread: only it waits for the deflate
+            ev_sizes.synchronize()
+            sz = sz_h.tolist()
+            cr = [c & 0xFFFFFFFF for c in cr_h.tolist()]
+            total = sum(sz)
+            with self.cv:
+                while self.pending > 0 and self.pending + total > self.cap:
+                    self.cv.wait()
+                self.pending += total
+            host = torch.empty(total, dtype=torch.uint8, pin_memory=True)
+            with torch.cuda.device(dev), torch.cuda.stream(side):
+                side.wait_event(ev_sizes)
+                o = 0
+                for i, n in enumerate(sz):  # the streams, back to back, one D2H each
+                    host[o:o + n].copy_(out[i * bound:i * bound + n], non_blocking=True)
+                    o += n
+                ev = torch.cuda.Event()
+                ev.record(side)
+            ev.synchronize()
+            o = 0
+            for i, n in enumerate(sz):
+                fut = self.pool.submit(write_one, host, i, o, n, cr[i])
+                fut.add_done_callback(lambda f, n=n: done(f, n))
+                with self._lock:
+                    self.futures.append(fut)
+                o += n
+
+        fut = self.fetcher.submit(fetch)
+        with self._lock:
             self.futures.append(fut)
-            o += n
 
     def save(self, path: str, **arrays) -> None:
         """NpzWriter.save's interface: the first device array is deflated on the
@@ -228,10 +269,17 @@ class GpuNpzWriter:
         self.save_batch([path], arrays[k0].unsqueeze(0), k0, extra)
 
     def flush(self) -> None:
-        futs, self.futures = self.futures, []
-        for f in futs:
-            f.result()
+        # a fetch job appends its files' jobs before it completes, so drain
+        # until no job is left
+        while True:
+            with self._lock:
+                futs, self.futures = self.futures, []
+            if not futs:
+                return
+            for f in futs:
+                f.result()
 
     def close(self) -> None:
         self.flush()
+        self.fetcher.shutdown()
         self.pool.shutdown()

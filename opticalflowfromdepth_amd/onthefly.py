@@ -276,6 +276,21 @@ class GlobalMatchFlowNet(nn.Module):
         return {"flow_preds": preds}
 
 
+def nan_on_any_rank(loss: torch.Tensor) -> bool:
+    """main.py:479-480 skips a step whose loss is NaN.  Under DDP with more
+    than one rank the skip must be collective: a rank that skipped backward
+    alone would leave the others blocked in the gradient all-reduce.  So the
+    NaN flag is all-reduced (MAX) and every rank skips together (the one
+    host sync of the step, as in the reference)."""
+    import torch.distributed as dist
+    nan = torch.isnan(loss.detach()).reshape(1).to(torch.float32)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        if dist.get_backend() == "gloo":
+            nan = nan.cpu()
+        dist.all_reduce(nan, op=dist.ReduceOp.MAX)
+    return bool(nan.item() > 0)
+
+
 def fetch_gmflow_optimizer(model, lr=4e-4, weight_decay=1e-4, num_steps=100):
     """adjusted_gmflow/main.py:230-231, :425-432: AdamW + cosine OneCycleLR."""
     opt = torch.optim.AdamW(model.parameters(), lr=lr, weight_decay=weight_decay)
@@ -301,7 +316,7 @@ def gmflow_train_step(model, optimizer, lr_scheduler, batch, device, args: StepA
         results = model(image1.float(), image2.float(), attn_splits_list=[2], corr_radius_list=[-1],
                         prop_radius_list=[-1])
     loss, metrics = flow_loss_func(results["flow_preds"], flow_gt, valid, gamma=args.gamma, max_flow=max_flow)
-    if torch.isnan(loss):
+    if nan_on_any_rank(loss):
         return None
     for p in model.parameters():  # :483-485
         p.grad = None

@@ -515,12 +515,19 @@ class PreprocessPlusAugment(nn.Module):
                 main.wait_stream(st)
 
     def run_batch(self, seeds: Sequence[int], img0, img0_depth, is_stereo=False, out_dirs=None,
-                  schedule: Sequence[int] = AUGMENT_SCHEDULE, augment=True):
+                  schedule: Sequence[int] = AUGMENT_SCHEDULE, augment=True, camera=None):
         """B images at once.  ``img0_depth`` is the raw depth (or the disparity
         when is_stereo, :352-353).  With ``out_dirs`` every image's npz files
-        are written like the reference; returns the group tensor [B,44,H,W]."""
+        are written like the reference; returns the group tensor [B,44,H,W].
+        ``camera`` = (s [B], T [B,4,4]) replaces the per-seed draws of the
+        camera scale and ego-motion (shard.broadcast_camera_params: rank 0's
+        draws, bit-identical to every rank's own)."""
         h, w = img0.shape[-2:]
         params = [draw_image_params(int(s), h, w, schedule) for s in seeds]
+        if camera is not None:
+            for p, s_i, T_i in zip(params, camera[0], camera[1]):
+                p["s"] = s_i.to(torch.float32)
+                p["T1"] = T_i.to(torch.float32)
         img0 = img0.to(self.device)
         d0 = img0_depth.to(self.device)
         if is_stereo:
@@ -673,16 +680,50 @@ def save_augment(out_dirs: Sequence[str], g: int, a: int, kind: int, d1: torch.T
 
 
 # ---------------------------------------------------------------- driver (preprocess.py:508-561)
-def main(argv=None) -> None:
+N_FILES_PER_IMAGE = 1 + 2 * N_GROUPS * len(AUGMENT_SCHEDULE)  # group.npz + 120 augmented pairs
+
+
+def image_complete(d: str, schedule: Sequence[int] = AUGMENT_SCHEDULE, augment: bool = True) -> bool:
+    """Every product file of one image exists (resume: --skip-existing)."""
+    names = ["group.npz"]
+    if augment:
+        names += [f"{g}_{a}_{k}.npz" for g in range(N_GROUPS) for a in range(len(schedule)) for k in (1, 2)]
+    return all(os.path.exists(os.path.join(d, n)) for n in names)
+
+
+def make_writer(kind: str):
+    """--writer: ``gpu`` (default) deflates on the GPU (npz_gpu.GpuNpzWriter),
+    ``zlib`` a 16-thread host zlib pool (NpzWriter, numpy's level 6),
+    ``sync`` the reference's synchronous np.savez_compressed (preprocess.py:446)."""
+    if kind == "gpu":
+        from .npz_gpu import GpuNpzWriter
+        return GpuNpzWriter(workers=int(os.environ.get("OFD_WRITER_WORKERS", "8")))
+    if kind == "zlib":
+        return NpzWriter(int(os.environ.get("OFD_WRITER_WORKERS", "16")), 6)
+    if kind == "sync":
+        return None
+    raise ValueError(f"unknown writer {kind!r}")
+
+
+def main(argv=None) -> dict:
     """``python -m opticalflowfromdepth_amd.preprocess`` -- the reference's
     ``__main__`` (preprocess.py:521-561) on synthetic depth maps (the DIML /
     ReDWeb readers are file I/O, out of scope): the same --gpu / --split /
     --split_id sharding (shard.shard_range), the same per-image seeds
     12345 + img_idx + epoch * N over two epochs, the same output tree
     (<out>/<img_idx + epoch * N>/group.npz and {g}_{a}_{1,2}.npz), B images
-    per batched call.  Under torchrun, --split / --split_id default to the
-    world size / rank (one process per GPU; no collective on the data path)."""
+    per batched call.  Under torchrun (WORLD_SIZE set) it joins a process
+    group (RCCL; OFD_PPA_BACKEND=gloo for CPU collectives), --split /
+    --split_id default to the world size / rank (one process per GPU), and the
+    camera parameters (s, T) of every image of an epoch come from rank 0 in
+    one broadcast (shard.broadcast_camera_params); the data path has no
+    collective.  The files are written by the GPU deflate writer by default
+    (--writer).  Returns (and prints as one JSON line) this rank's images,
+    files, bytes and images/s with every file written."""
     import argparse
+    import json
+    import time
+    import torch.distributed as dist
     from . import shard
     ap = argparse.ArgumentParser()
     ap.add_argument("--dataset", default="synthetic", choices=["synthetic"])
@@ -693,30 +734,76 @@ def main(argv=None) -> None:
     ap.add_argument("--split", default=None, type=int)
     ap.add_argument("--split_id", default=None, type=int)
     ap.add_argument("--epochs", default=2, type=int)
-    ap.add_argument("--batch", default=64, type=int,
-                    help="images per batched call (larger batches amortise the hole-fill layer latency)")
+    ap.add_argument("--batch", default=8, type=int,
+                    help="images per batched call (larger batches amortise the hole-fill latency; the writer "
+                         "bounds the product at any batch)")
     ap.add_argument("--out", default="datasets/AugmentedDatasets/synthetic")
+    ap.add_argument("--writer", default="gpu", choices=["gpu", "zlib", "sync"])
+    ap.add_argument("--skip-existing", action="store_true", help="resume: skip images whose 121 files exist")
     ap.add_argument("--no-augment", action="store_true")
     ap.add_argument("--no-save", action="store_true")
     a = ap.parse_args(argv)
+    launched = "WORLD_SIZE" in os.environ
     world, rank = int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0"))
     split = a.split if a.split is not None else world
     split_id = a.split_id if a.split_id is not None else rank
     gpu = a.gpu if a.gpu is not None else int(os.environ.get("LOCAL_RANK", "0"))
     dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
+    backend = os.environ.get("OFD_PPA_BACKEND", "nccl")
+    if launched and not dist.is_initialized():
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    coll_dev = dev if backend == "nccl" else torch.device("cpu")
     N, h, w = a.n_images, a.height, a.width
     start, end = shard.shard_range(N, split, split_id)
+    writer = None if a.no_save else make_writer(a.writer)
     ppa = PreprocessPlusAugment(dev)
-    for epoch in range(a.epochs):
-        for b0 in range(start, end, a.batch):
-            idx = list(range(b0, min(b0 + a.batch, end)))
-            seeds = [shard.image_seed(i, epoch, N) for i in idx]
-            img0 = synth.synthetic_rgb(seeds, h, w, dev)
-            depth = synth.synthetic_depth(seeds, h, w, dev, dtype=torch.float64)  # utils.get_depth is float64
-            dirs = None if a.no_save else [os.path.join(a.out, str(i + epoch * N)) for i in idx]
-            ppa.run_batch(seeds, img0, depth, out_dirs=dirs, augment=not a.no_augment)
-            print(f"rank {rank}: epoch {epoch} images {idx[0]}..{idx[-1]} done", flush=True)
+    ppa.writer = writer
+    done = skipped = 0
+    t0 = time.perf_counter()
+    try:
+        for epoch in range(a.epochs):
+            # every rank takes part in the broadcast of the whole epoch's camera
+            # parameters (17 floats per image), then keeps its own shard's
+            seeds_all = [shard.image_seed(i, epoch, N) for i in range(N)]
+            s_all, T_all = shard.broadcast_camera_params(seeds_all, device=coll_dev)
+            todo = list(range(start, end))
+            if a.skip_existing and not a.no_save:
+                keep = [i for i in todo if not image_complete(os.path.join(a.out, str(i + epoch * N)),
+                                                              augment=not a.no_augment)]
+                skipped += len(todo) - len(keep)
+                todo = keep
+            for b0 in range(0, len(todo), a.batch):
+                idx = todo[b0:b0 + a.batch]
+                seeds = [seeds_all[i] for i in idx]
+                img0 = synth.synthetic_rgb(seeds, h, w, dev)
+                depth = synth.synthetic_depth(seeds, h, w, dev, dtype=torch.float64)  # utils.get_depth is float64
+                dirs = None if a.no_save else [os.path.join(a.out, str(i + epoch * N)) for i in idx]
+                ppa.run_batch(seeds, img0, depth, out_dirs=dirs, augment=not a.no_augment,
+                              camera=(s_all[idx], T_all[idx]))
+                done += len(idx)
+                print(f"rank {rank}: epoch {epoch} images {idx[0]}..{idx[-1]} done", flush=True)
+        if writer is not None:
+            writer.flush()
+        torch.cuda.synchronize(dev)
+    finally:
+        if writer is not None and hasattr(writer, "close"):
+            writer.close()
+    el = time.perf_counter() - t0
+    rep = {"rank": rank, "split": split, "split_id": split_id, "shard": [start, end], "epochs": a.epochs,
+           "images": done, "skipped": skipped, "height": h, "width": w, "batch": a.batch,
+           "writer": None if a.no_save else a.writer,
+           "files": 0 if a.no_save else done * (N_FILES_PER_IMAGE if not a.no_augment else 1),
+           "bytes_written": getattr(writer, "bytes_written", None), "seconds": round(el, 3),
+           "images_per_s": round(done / el, 3) if el > 0 else None}
+    print(json.dumps(rep), flush=True)
+    if launched and dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()
+    return rep
 
 
 if __name__ == "__main__":

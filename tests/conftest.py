@@ -10,6 +10,15 @@ if REPO not in sys.path:
 GOLDEN = os.path.join(REPO, "tests", "golden")
 
 
+def pytest_report_header(config):
+    # which library the run is testing: the build id is the hash of the sources
+    try:
+        from opticalflowfromdepth_amd import _native, build
+        return f"libofd_fw build id {_native.build_id()} (sources {build.source_hash()})"
+    except Exception as e:  # noqa: BLE001 -- a header must never fail the run
+        return f"libofd_fw not loaded: {e}"
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device); run with -m gpu")
 

@@ -178,6 +178,40 @@ def test_gmflow_step_skips_nan_loss():
         assert torch.equal(v, before[k]), k
 
 
+def _nan_skip_target(rank, world, outdir, port):
+    """Rank 1's first batch makes a NaN loss, rank 0's does not: under DDP both
+    must skip that step together, then both take the next one."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    model = torch.nn.parallel.DistributedDataParallel(otf.GlobalMatchFlowNet(dim=16))
+    opt, sched = otf.fetch_gmflow_optimizer(model, num_steps=4)
+    nan_ops = otf.PairOps(warp=_cpu_ops().warp,
+                          ego_flow=lambda d, T: torch.full_like(d.expand(-1, 2, -1, -1), float("nan")),
+                          fill=_cpu_ops().fill)
+    bs = _batches(rank, world, 2, 2)
+    if rank == 1:
+        bs[0][4][:] = 1  # ego-motion images only: every flow is NaN
+    r1 = otf.gmflow_train_step(model, opt, sched, bs[0], "cpu", otf.StepArgs(gamma=0.9, amp=False),
+                               nan_ops if rank == 1 else _cpu_ops())
+    r2 = otf.gmflow_train_step(model, opt, sched, bs[1], "cpu", otf.StepArgs(gamma=0.9, amp=False), _cpu_ops())
+    sd = {k: v.detach().cpu() for k, v in model.module.state_dict().items()}
+    torch.save({"params": sd, "first": r1 is None, "second": r2 is not None, "epoch": sched.last_epoch},
+               os.path.join(outdir, f"nan{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_gmflow_nan_skip_is_collective_under_ddp(tmp_path):
+    mp.spawn(_nan_skip_target, args=(2, str(tmp_path), 29737), nprocs=2, join=True)
+    r0, r1 = (torch.load(tmp_path / f"nan{r}.pt", weights_only=True) for r in range(2))
+    assert r0["first"] and r1["first"]          # both skipped the step rank 1's NaN poisoned
+    assert r0["second"] and r1["second"]        # and both took the next one
+    assert r0["epoch"] == r1["epoch"] == 1
+    for k in r0["params"]:
+        assert torch.equal(r0["params"][k], r1["params"][k]), k
+
+
 def test_ddp_gloo_world2_matches_single_process(tmp_path):
     per_rank, steps = 2, 2
     mp.spawn(_spawn_target, args=(2, per_rank, steps, str(tmp_path), 29731, "cpu"), nprocs=2, join=True)
