@@ -101,6 +101,14 @@ int ofd_fw_set_engine(int engine);
  * queries.  Returns the previous setting.  Process-wide, not thread-safe. */
 int ofd_fw_set_disparity_rows(int on);
 
+/* Short TILE-engine calls -- fewer than `tiles_per_slot` target tiles per
+ * resident SPLAT workgroup -- run one SPLAT workgroup per tile instead of the
+ * persistent SPLAT (default 16, also OFD_PERSIST_MIN); 0 = always persistent
+ * (tests drive the persistent kernel's queues on small images with it).
+ * Results are identical.  A negative value only queries.  Returns the
+ * previous setting.  Process-wide, not thread-safe against concurrent calls. */
+int ofd_fw_set_persist_min(int tiles_per_slot);
+
 /* Benchmark hook: when non-NULL, the given hipEvent_t's are recorded on the
  * launch stream right before the first and right after the last launch of
  * each subsequent f32 call's dominant kernel: SPLAT (TILE engine), RESOLVE

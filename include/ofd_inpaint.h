@@ -104,6 +104,14 @@ int ofd_inpaint_set_schedule(int launch_layers, int thin_cap);
  * clears them.  Returns the bits (>= 0) or -1 on a HIP error. */
 int ofd_inpaint_faults(int reset);
 
+/* Diagnostic: how many hole layers the layered fill's one-workgroup deep-tail
+ * kernel has run since the last reset (layers deeper than the launches the
+ * host sized from recent calls at the shape -- a call much deeper than the
+ * last 8 at its shape).  Those layers run 16 parts one after another on one
+ * CU: results are unchanged, time is not.  Blocking; reset != 0 clears the
+ * count.  Returns the count (>= 0) or -1 on a HIP error. */
+int ofd_inpaint_tail_layers(int reset);
+
 #ifdef __cplusplus
 }
 #endif

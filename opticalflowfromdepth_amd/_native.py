@@ -34,6 +34,7 @@ SIGNATURES = {
     "ofd_fw_strerror": ([ctypes.c_int], ctypes.c_char_p),
     "ofd_fw_set_engine": ([ctypes.c_int], ctypes.c_int),
     "ofd_fw_set_disparity_rows": ([ctypes.c_int], ctypes.c_int),
+    "ofd_fw_set_persist_min": ([ctypes.c_int], ctypes.c_int),
     "ofd_fw_set_profile_events": ([_P, _P], ctypes.c_int),
     "ofd_fw_workspace_bytes": ([_I64, _I64, _I64, ctypes.c_int], _SZ),
     "ofd_fw_workspace_init": ([_P, _SZ, _P], ctypes.c_int),
@@ -56,6 +57,7 @@ SIGNATURES = {
     "ofd_inpaint_telea_seq_f32": ([_P] * 4 + [_I64] * 4 + [ctypes.c_int, _P, _SZ, _P], ctypes.c_int),
     "ofd_inpaint_set_schedule": ([ctypes.c_int, ctypes.c_int], ctypes.c_int),
     "ofd_inpaint_faults": ([ctypes.c_int], ctypes.c_int),
+    "ofd_inpaint_tail_layers": ([ctypes.c_int], ctypes.c_int),
     "ofd_deflate_bound": ([_I64], _SZ),
     "ofd_deflate_workspace_bytes": ([_I64, _I64], _SZ),
     "ofd_deflate_batch": ([_P, _I64, _I64, _P, _P, _P, _P, _SZ, _P], ctypes.c_int),
@@ -99,6 +101,8 @@ def lib():
         except OSError as e:
             raise NativeLibraryError(f"cannot load {LIB_PATH}: {e}") from e
         for name, (argt, rest) in SIGNATURES.items():
+            if override and not hasattr(l, name):
+                continue  # a probe build from older sources may lack newer entry points
             fn = getattr(l, name)
             fn.argtypes = argt
             fn.restype = rest

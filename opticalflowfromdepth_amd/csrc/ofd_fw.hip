@@ -1653,12 +1653,14 @@ unsigned persist_grid(unsigned tiles) {
 // persistent; config 5 (64 x 368x560, 7.5) 0.218 vs 0.234; 32 x 768x1024 (12)
 // 0.383 vs 0.387; 16 x 768x1024 (6) 0.218 vs 0.216; the headline (24) 0.741
 // vs 0.721 -- the persistent queues pay off only on long calls.
+int g_persist_min = -1;  // ofd_fw_set_persist_min; -1 = not set (OFD_PERSIST_MIN, else 16)
 unsigned persist_min() {
-    static const unsigned v = [] {
+    if (g_persist_min < 0) {
         const char *e = getenv("OFD_PERSIST_MIN");
-        return e ? unsigned(atoi(e)) : 16u;
-    }();
-    return v;
+        g_persist_min = e ? atoi(e) : 16;
+        if (g_persist_min < 0) g_persist_min = 16;
+    }
+    return unsigned(g_persist_min);
 }
 
 // Optional timing hook (ofd_fw_set_profile_events): events recorded on the
@@ -1920,6 +1922,12 @@ int ofd_fw_set_profile_events(void *start_event, void *stop_event) {
 int ofd_fw_set_disparity_rows(int on) {
     const int prev = disp_row_enabled() ? 1 : 0;
     if (on == 0 || on == 1) g_disp_rows = on;
+    return prev;
+}
+
+int ofd_fw_set_persist_min(int tiles_per_slot) {
+    const int prev = int(persist_min());
+    if (tiles_per_slot >= 0) g_persist_min = tiles_per_slot;
     return prev;
 }
 

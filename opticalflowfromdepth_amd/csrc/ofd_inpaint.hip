@@ -60,6 +60,8 @@
 // waits on another workgroup, so it has no bit of its own (bits 1-2 are the
 // sequential fill's).
 __device__ unsigned g_ip_fault;
+// layers run by the deep-tail kernel (ofd_inpaint_tail_layers)
+__device__ unsigned g_ip_tail_layers;
 
 unsigned ofd_sq_fault_read(int reset);  // ofd_inpaint_seq.hip
 
@@ -1214,6 +1216,7 @@ __global__ __launch_bounds__(256) void ip_hole_tail_kernel(Chunk ch, const uint3
                                                            int nring, unsigned L0, int range, unsigned thin_cap) {
     __shared__ WavePatch patch[4];
     const unsigned lmax = meta[0];
+    if (threadIdx.x == 0 && lmax >= L0) atomicAdd(&g_ip_tail_layers, lmax - L0 + 1u);
     for (unsigned L = L0; L <= lmax; ++L) {
         for (unsigned bx = 0; bx < kTailParts; ++bx)
             hole_layer_body(ch, list, hist, cursor, nring, L, range, thin_cap, patch, bx, kTailParts);
@@ -1330,6 +1333,16 @@ LaggedStats &lagged_stats(int64_t nb, int64_t H, int64_t W, int r) {
 }  // namespace
 
 extern "C" {
+
+int ofd_inpaint_tail_layers(int reset) {
+    unsigned v = 0;
+    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_ip_tail_layers), sizeof(v)) != hipSuccess) return -1;
+    if (reset) {
+        const unsigned z = 0;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_ip_tail_layers), &z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return int(v);
+}
 
 int ofd_inpaint_faults(int reset) {
     unsigned v = 0;

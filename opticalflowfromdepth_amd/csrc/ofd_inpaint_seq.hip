@@ -1672,6 +1672,10 @@ __global__ __launch_bounds__(256, OFD_REC_MINW) void sq_record3_kernel(SqWs w) {
     }
 }
 
+#ifndef OFD_C3_PF  // probe knob: 0 = append at the level's end (base); 1 / 2 = append + record touch earlier
+#define OFD_C3_PF 0
+#endif
+
 struct C3Lds {
     uint32_t nnext[3];  // level l appends to nnext[l % 3]; reset two levels ahead (one barrier per level)
     uint64_t fr[2][kFrCap];
@@ -1772,6 +1776,31 @@ __global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, int C, int H, 
                     old[k] = atomicSub(&m.own[q], 1u);
                 }
             }
+            uint32_t pfv[8], pfw[8];  // OFD_C3_PF: record touches (values never used)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) pfv[k] = pfw[k] = 0u;
+            // the holes whose last earlier neighbour this was join the next
+            // level; OFD_C3_PF > 0 (probe): appended earlier in the level, and
+            // each one's record lines touched then, so the next level's record
+            // loads hit L2 (the touch overlaps the rest of this level)
+            auto append_ready = [&]() {
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    if ((old[k] & 63u) == 1u) {
+                        const uint32_t f = atomicAdd(&L.nnext[lv], 1u);
+                        const int64_t q = int64_t(p) + int64_t(WC(k) / 9 - 4) * ew + (WC(k) % 9 - 4);
+                        const uint64_t en = (uint64_t(old[k] >> 6) << 32) | uint64_t(q);
+                        if (f < uint32_t(kFrCap))
+                            L.fr[cur ^ 1][f] = en;
+                        else
+                            gb[f] = en;
+                        if (OFD_C3_PF) {  // plain loads, consumed only at the round's end
+                            const uint32_t *rq = m.rec + size_t(old[k] >> 6) * kRecW;
+                            pfv[k] = rq[0];
+                            pfw[k] = rq[kRecW - 1];
+                        }
+                    }
+            };
             SQ_T(c1);
             // this lane's terms (disk positions gl + 8k): channels 1 and 2 go
             // to LDS at once (past the grid), channel 0 waits in registers
@@ -1829,6 +1858,7 @@ __global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, int C, int H, 
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (OFD_C3_PF == 1) append_ready();
             SQ_T(c2);
             // cv2's sums in its (k, l) order: chains gl and gl + 8 side by side
             // (independent accumulators; Ia chains add, Jx / Jy chains subtract)
@@ -1850,6 +1880,7 @@ __global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, int C, int H, 
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             SQ_T(c3);
+            if (OFD_C3_PF == 2) append_ready();
             if (act && gl < C) {
                 const float sum = __uint_as_float(mq.z);
                 const float Ia = L.res[g][3 * gl], Jx = L.res[g][3 * gl + 1], Jy = L.res[g][3 * gl + 2];
@@ -1860,20 +1891,14 @@ __global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, int C, int H, 
                 shb[4 * (int64_t(i - 1) * W + (j - 1)) + gl] = uint8_t(u);
             }
             // holes whose last earlier neighbour this was join the next level
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-                if ((old[k] & 63u) == 1u) {
-                    const uint32_t f = atomicAdd(&L.nnext[lv], 1u);
-                    const int64_t q = int64_t(p) + int64_t(WC(k) / 9 - 4) * ew + (WC(k) % 9 - 4);
-                    const uint64_t en = (uint64_t(old[k] >> 6) << 32) | uint64_t(q);
-                    if (f < uint32_t(kFrCap))
-                        L.fr[cur ^ 1][f] = en;
-                    else
-                        gb[f] = en;
-                }
+            if (OFD_C3_PF == 0) append_ready();
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (OFD_C3_PF) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) asm volatile("" ::"v"(pfv[k]), "v"(pfw[k]));
+            }
             SQ_T(c4);
             SQ_ACC(2, c0, c0a);
             SQ_ACC(6, c0a, c1);

@@ -497,7 +497,7 @@ def _tol_channels(key, kind):
     return (4, 5, 6, 7) if key.endswith("_1") else (0, 1, 2, 3)
 
 
-def make_ppa_fill_cases(utils_mod, ref_fw, Convert):
+def make_ppa_fill_cases(utils_mod, ref_fw, Convert, h=32, w=40, seeds=(5150, 5151), sample=(5, 7), tol_full=True):
     """PreprocessPlusAugment.forward (:329-476) of two 32x40 images with the
     real hole-fill: the reference's text slices run with utils.inpaint backed
     by _Cv2Telea (cv2's sequential Telea, restated by the oracle), the oracle
@@ -505,7 +505,11 @@ def make_ppa_fill_cases(utils_mod, ref_fw, Convert):
     digest of the channel (bit-exact bar), plus the float32 values of the
     channels held to the 1e-5 px geometry tolerance, and a strided sample of
     every channel for readable failures.  ``holes`` counts the pixels each
-    image's 95 fills actually filled (the fill is not idle)."""
+    image's 95 fills actually filled (the fill is not idle).
+
+    ``tol_full=False`` (the larger-image fixture, ppa_fill_large.npz) keeps
+    the tolerance channels as a strided sample plus their sum and absolute
+    sum instead of whole planes, so the fixture stays a few MB."""
     import tempfile
     import torch.nn as nn
     lines = open(os.path.join(REF, "preprocess.py")).read().split("\n")
@@ -517,12 +521,10 @@ def make_ppa_fill_cases(utils_mod, ref_fw, Convert):
     for a, b in ((301, 326), (24, 182)):
         exec(compile("\n".join(lines[a - 1:b]), os.path.join(REF, "preprocess.py"), "exec"), ns)
     exec(compile("\n".join(body), os.path.join(REF, "preprocess.py"), "exec"), ns)
-    h, w = 32, 40
-    cases = {"h": np.array(h), "w": np.array(w)}
+    cases = {"h": np.array(h), "w": np.array(w), "sample_stride": np.array(sample)}
     ref_inpaint, tel = load_reference_inpaint(_Cv2Telea)
     utils_mod.inpaint = lambda img, valid, coll: ref_inpaint(img.as_subclass(_CpuImage), valid, coll).as_subclass(
         torch.Tensor)
-    seeds = (5150, 5151)
     cases["seeds"] = np.array(seeds)
     for n, seed in enumerate(seeds):
         raw = synth_depth(h, w, seed)
@@ -550,9 +552,13 @@ def make_ppa_fill_cases(utils_mod, ref_fw, Convert):
             if kind is not None:
                 cases[pre + "/type"] = np.array(kind)
             cases[pre + "/digest"] = np.array([_digest(arr[c]) for c in range(arr.shape[0])])
-            cases[pre + "/sample"] = np.ascontiguousarray(arr[:, ::5, ::7]).astype(np.float32)
+            cases[pre + "/sample"] = np.ascontiguousarray(arr[:, ::sample[0], ::sample[1]]).astype(np.float32)
             for c in _tol_channels(key, kind):
-                cases[f"{pre}/tol{c}"] = arr[c].astype(np.float32)
+                if tol_full:
+                    cases[f"{pre}/tol{c}"] = arr[c].astype(np.float32)
+                else:
+                    cases[f"{pre}/tolsum{c}"] = np.array([arr[c].astype(np.float64).sum(),
+                                                         np.abs(arr[c].astype(np.float64)).sum()])
     return cases
 
 
@@ -612,6 +618,12 @@ def main():
         pf = make_ppa_fill_cases(utils_mod, ref_fw, Convert)
         np.savez_compressed(os.path.join(HERE, "ppa_fill.npz"), **pf)
         print("ppa_fill.npz", os.path.getsize(os.path.join(HERE, "ppa_fill.npz")), "bytes")
+        return
+    if sys.argv[1:] == ["ppa_fill_large"]:  # one 192x256 image: ego-motion border bands, larger fills
+        pf = make_ppa_fill_cases(utils_mod, ref_fw, Convert, h=192, w=256, seeds=(5160,), sample=(8, 8),
+                                 tol_full=False)
+        np.savez_compressed(os.path.join(HERE, "ppa_fill_large.npz"), **pf)
+        print("ppa_fill_large.npz", os.path.getsize(os.path.join(HERE, "ppa_fill_large.npz")), "bytes")
         return
     if sys.argv[1:] == ["ppa_forward"]:  # only the per-image forward fixture
         ref_inpaint, rec = load_reference_inpaint()

@@ -11,6 +11,8 @@
 """
 import os
 
+import time
+
 import numpy as np
 import pytest
 import torch
@@ -247,6 +249,52 @@ def test_inpaint_layered_deep_ego_layers_every_schedule():
             assert bad.size == 0, f"{sched}: {len(bad)} differing, first {bad[:5].tolist()}"
     finally:
         lib.ofd_inpaint_set_schedule(-1, -1)
+    assert lib.ofd_inpaint_faults(1) == 0
+
+
+@pytest.mark.gpu
+def test_inpaint_layered_deep_call_after_shallow_history():
+    """the launch schedule is sized from the last 8 calls at a
+    shape, so a deep call after 8 shallow ones runs its extra layers in the
+    one-workgroup tail (ofd_inpaint_tail_layers counts them).  Results stay
+    the layered oracle's bits; the count shows the cliff is taken, and a
+    second deep call (now in the history) takes none.  tools/tail_cliff.py
+    times the same sequence."""
+    from opticalflowfromdepth_amd import _native, forward_warp_flow, ops, shard, synth
+    lib = _native.lib()
+    dev = torch.device("cuda:0")
+    H, W = 384, 512
+    seeds = [shard.image_seed(i) for i in range(2)]
+    shallow = synth.stage_one_batch(seeds, H, W, dev, ego_fraction=0.0)  # disparity flows: thin holes
+    deep = synth.stage_one_batch(seeds, H, W, dev, ego_fraction=1.0)     # ego-motion: deep border bands
+
+    def fill_inputs(batch):
+        out, valid, coll = forward_warp_flow(*batch)
+        return (out[:, 0:3] * valid).contiguous(), valid, coll
+
+    s_in, d_in = fill_inputs(shallow), fill_inputs(deep)
+    exp = oracle.inpaint(*(t.cpu().numpy() for t in d_in), 3, layered=True)
+    lib.ofd_inpaint_set_schedule(-1, -1)
+    for _ in range(10):
+        ops.inpaint(*s_in, order="layered")
+    torch.cuda.synchronize()
+    time.sleep(0.05)  # let the statistics copies land (they are read only once complete)
+    ops.inpaint(*s_in, order="layered")
+    torch.cuda.synchronize()
+    lib.ofd_inpaint_tail_layers(1)
+    got = ops.inpaint(*d_in, order="layered")
+    torch.cuda.synchronize()
+    n_cliff = lib.ofd_inpaint_tail_layers(1)
+    assert np.array_equal(got.cpu().numpy(), exp)
+    assert n_cliff > 0
+    time.sleep(0.05)
+    ops.inpaint(*d_in, order="layered")
+    torch.cuda.synchronize()
+    lib.ofd_inpaint_tail_layers(1)
+    got2 = ops.inpaint(*d_in, order="layered")
+    torch.cuda.synchronize()
+    assert lib.ofd_inpaint_tail_layers(1) == 0
+    assert np.array_equal(got2.cpu().numpy(), exp)
     assert lib.ofd_inpaint_faults(1) == 0
 
 
