@@ -33,7 +33,7 @@
  *       call); caller-owned scratch, no initialisation needed.
  *   ofd_inpaint_set_schedule
  *       no reference counterpart: diagnostics / tests only (how many hole
- *       layers are launched one by one before the one-workgroup deep-tail
+ *       layers are launched one by one before the deep-tail
  *       kernel takes over, and the layer size below which every hole takes the
  *       wave-per-hole path).  Results never depend on it.
  *
@@ -89,27 +89,28 @@ int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float 
                               size_t workspace_bytes, void *stream);
 
 /* Diagnostics: launch_layers >= 0 launches exactly that many hole layers one
- * by one (the one-workgroup deep-tail kernel does the rest); thin_cap >= 0 sets the layer
+ * by one (the deep-tail kernel does the rest); thin_cap >= 0 sets the layer
  * size up to which every hole takes the wave path.  -1 restores the
  * defaults (launches sized from an earlier call's depth; thin_cap 4096).
  * Process-wide; returns 0. */
 int ofd_inpaint_set_schedule(int launch_layers, int thin_cap);
 
 /* Test / debug hook: the OR of the invariant-violation bits any hole-fill
- * kernel raised since the last reset (the layered fill waits on nothing and
- * raises none) -- 2: a sequential-march bucket index passed its bound; 4: a sequential
- * distance sweep passed its iteration bound.  Each is unreachable while the
+ * kernel raised since the last reset -- 2: a sequential-march bucket index
+ * passed its bound; 4: a sequential distance sweep passed its iteration bound;
+ * 8: the layered fill's deep tail gave up waiting for a previous layer.  Each is unreachable while the
  * algorithm's invariants hold, and each means that call's output is
  * incomplete.  Blocking (a device-to-host copy of the fault words); reset != 0
  * clears them.  Returns the bits (>= 0) or -1 on a HIP error. */
 int ofd_inpaint_faults(int reset);
 
-/* Diagnostic: how many hole layers the layered fill's one-workgroup deep-tail
- * kernel has run since the last reset (layers deeper than the launches the
- * host sized from recent calls at the shape -- a call much deeper than the
- * last 8 at its shape).  Those layers run 16 parts one after another on one
- * CU: results are unchanged, time is not.  Blocking; reset != 0 clears the
- * count.  Returns the count (>= 0) or -1 on a HIP error. */
+/* Diagnostic: how many hole layers the layered fill's deep-tail kernel has
+ * run since the last reset (layers deeper than the launches the host sized
+ * from recent calls at the shape -- a call much deeper than the last 8 at its
+ * shape).  The tail runs them on a small persistent grid, layer after layer
+ * (a wait per layer instead of a launch): results are unchanged.  Blocking;
+ * reset != 0 clears the count.  Returns the count (>= 0) or -1 on a HIP
+ * error. */
 int ofd_inpaint_tail_layers(int reset);
 
 #ifdef __cplusplus

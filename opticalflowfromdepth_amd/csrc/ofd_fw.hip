@@ -168,9 +168,6 @@ __device__ __forceinline__ void load4(const T *__restrict__ q, T v[4], int n) {
         ty1 = ty0;                                                                                    \
     }
 
-#ifndef OFD_PROBE_NODEPTH  // timing probe only: SPLAT skips the depth plane (wrong winners)
-#define OFD_PROBE_NODEPTH 0
-#endif
 // Coordinate sources whose z-test depth is the separate float32 depth plane
 // and that generate no obj channels.
 #define KEY_DEPTH_FROM_PLANE                                                                            \
@@ -179,8 +176,7 @@ __device__ __forceinline__ void load4(const T *__restrict__ q, T v[4], int n) {
     __device__ __forceinline__ void load4d(int64_t b, int64_t p, V x[4], V y[4], float dk[4], int n,  \
                                            const float *depth) const {                                \
         load4<kVec>(b, p, x, y, n);                                                                   \
-        if (OFD_PROBE_NODEPTH) { for (int e = 0; e < 4; ++e) dk[e] = 1.0f + float(p & 7); }          \
-        else ::load4<kVec>(depth + b * HW + p, dk, n);                                                \
+        ::load4<kVec>(depth + b * HW + p, dk, n);                                                     \
     }                                                                                                 \
     __device__ __forceinline__ float key_depth(int64_t b, int64_t p, const float *depth) const {     \
         return depth[b * HW + p];                                                                     \
@@ -883,23 +879,6 @@ __device__ __forceinline__ void band_major_tile(unsigned lin, int nimg, const Ti
     }
 }
 
-// Quad publish (16-byte stores of 4 consecutive targets; probe builds set 0)
-#ifndef OFD_PUB4
-#define OFD_PUB4 0
-#endif
-typedef float F4 __attribute__((ext_vector_type(4)));
-typedef unsigned short U16x4 __attribute__((ext_vector_type(4)));
-template <typename E>
-struct Quad;
-template <>
-struct Quad<float> {
-    using type = F4;
-};
-template <>
-struct Quad<unsigned short> {
-    using type = U16x4;
-};
-
 // What SPLAT writes.  Split engine: valid, collision and the winner map (the
 // workspace's); fused engine (kFuse): valid, collision and the C output
 // planes, gathered from obj right out of the LDS z-buffer.
@@ -1188,63 +1167,6 @@ __device__ __forceinline__ void splat_tile(TileLds &L, unsigned lin, int bl, int
         E *oo = static_cast<E *>(io.out) + b * int64_t(C) * HW;
         const unsigned uHW = unsigned(HW);
         auto source = [&](int c, unsigned wi) -> E { return ob[unsigned(c) * uHW + wi]; };
-        if constexpr (kVec && OFD_PUB4) {
-            // Quad publish: a thread owns runs of 4 consecutive targets of a
-            // tile row and writes every plane with one 16-byte store per run
-            // (8 bytes for bf16) -- a quarter of the store instructions of
-            // the one-target-per-lane publish.  kVec guarantees W % 4 == 0
-            // and 16-byte aligned planes, so a run is wholly inside or
-            // wholly outside the image.
-            using E4 = typename Quad<E>::type;
-            constexpr int kQ = kT / 4 > 0 ? kT / 4 : 1;
-            constexpr int kQW = TW / 4;  // runs per tile row
-#pragma unroll
-            for (int k = 0; k < TW * TH / 4 / Cfg::kThr; k += kQ) {
-                unsigned t[kQ], w[kQ][4];
-                bool in[kQ];
-#pragma unroll
-                for (int u = 0; u < kQ; ++u) {
-                    const int q = int(threadIdx.x) + (k + u) * Cfg::kThr;
-                    const int ly = q / kQW, lx = (q - ly * kQW) * 4;
-                    const int ty = y0 + ly, tx = x0 + lx;
-                    in[u] = ty < H && tx < W;
-                    const ulonglong2 *zp = reinterpret_cast<const ulonglong2 *>(&L.zk[ly * TW + lx]);
-                    const ulonglong2 k01 = zp[0], k23 = zp[1];
-                    const unsigned long long key[4] = {k01.x, k01.y, k23.x, k23.y};
-                    F4 vv, cv;
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const bool touched = key[e] != KEY_UNTOUCHED;
-                        const bool nowin = key[e] == KEY_NOWIN;
-                        vv[e] = touched ? 1.f : 0.f;
-                        cv[e] = nowin ? 1.f : 0.f;
-                        w[u][e] = (in[u] && touched && !nowin) ? unsigned(key[e] & 0xFFFFFFFFull) : WIN_NONE;
-                    }
-                    t[u] = unsigned(ty) * unsigned(W) + unsigned(tx);
-                    if (in[u]) {
-                        __builtin_nontemporal_store(vv, reinterpret_cast<F4 *>(vb + t[u]));
-                        __builtin_nontemporal_store(cv, reinterpret_cast<F4 *>(cb + t[u]));
-                    }
-                }
-                for (int c0 = 0; c0 < C; c0 += kCh) {
-                    E4 o[kQ][kCh];
-#pragma unroll
-                    for (int u = 0; u < kQ; ++u)
-#pragma unroll
-                        for (int cc = 0; cc < kCh; ++cc)
-#pragma unroll
-                            for (int e = 0; e < 4; ++e)
-                                o[u][cc][e] = (w[u][e] != WIN_NONE && c0 + cc < C) ? source(c0 + cc, w[u][e]) : E(0);
-#pragma unroll
-                    for (int u = 0; u < kQ; ++u)
-#pragma unroll
-                        for (int cc = 0; cc < kCh; ++cc)
-                            if (in[u] && c0 + cc < C)
-                                __builtin_nontemporal_store(
-                                    o[u][cc], reinterpret_cast<E4 *>(oo + unsigned(c0 + cc) * uHW + t[u]));
-                }
-            }
-        } else {
 #pragma unroll
         for (int k = 0; k < TW * TH / Cfg::kThr; k += kT) {
             unsigned t[kT], w[kT];
@@ -1281,7 +1203,6 @@ __device__ __forceinline__ void splat_tile(TileLds &L, unsigned lin, int bl, int
                         if (in[u] && c0 + cc < C)
                             __builtin_nontemporal_store(o[u][cc], oo + unsigned(c0 + cc) * uHW + t[u]);
             }
-        }
         }
     } else {
         unsigned int *win = ws.winner + int64_t(bl) * HW;
@@ -1705,10 +1626,7 @@ int run_f32(Coords co, const E *obj, const float *depth, E *out, float *valid, f
     }
     const Ws slab = carve(ws, G, HW, g);
     // 16-byte coordinate / depth loads in BIN and SPLAT
-    // (and, fused TILE engine, the quad publish's 16-byte stores: output
-    // planes and masks 16-byte aligned too)
-    const bool vec = W % 4 == 0 && co.vec_ok() && uintptr_t(depth) % 16 == 0 && aligned(out, 16) &&
-                     aligned(valid, 16) && aligned(coll, 16);
+    const bool vec = W % 4 == 0 && co.vec_ok() && uintptr_t(depth) % 16 == 0;
     for (int64_t c = 0; c < nch; ++c) {
         const int64_t b0 = c * G;
         const int64_t nb = (B - b0) < G ? (B - b0) : G;

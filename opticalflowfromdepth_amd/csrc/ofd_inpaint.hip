@@ -30,7 +30,7 @@
 //          histograms, one scan, one scatter); the counts stay on the device.
 //   LAYERS one launch per outer-band layer and per hole layer over every
 //          image of the chunk, each reading its layer's size and offset from
-//          the device; a one-workgroup tail kernel runs any layer deeper
+//          the device; a persistent deep-tail kernel runs any layer deeper
 //          than the launches (no inter-workgroup waits anywhere).  Grids and the number of
 //          launches come from recent calls' counts read back asynchronously
 //          (LaggedStats): the host never waits.
@@ -56,9 +56,11 @@
 
 #pragma clang fp contract(off)
 
-// Fault word of the layered fill (ofd_inpaint_faults): no layered kernel
-// waits on another workgroup, so it has no bit of its own (bits 1-2 are the
-// sequential fill's).
+// Fault word of the layered fill (ofd_inpaint_faults): bit 8 = the deep
+// tail's wait for a previous layer passed its bound (unreachable: every part
+// it waits for is held by a running workgroup; the wait gives up rather than
+// hang, and the output is then incomplete).  Bits 1-2 are the sequential
+// fill's.
 __device__ unsigned g_ip_fault;
 // layers run by the deep-tail kernel (ofd_inpaint_tail_layers)
 __device__ unsigned g_ip_tail_layers;
@@ -736,6 +738,8 @@ __global__ __launch_bounds__(1024) void ip_scan_kernel(const unsigned *__restric
     }
     if (tid == 0) {
         meta[0] = lmax;
+        meta[1] = 0u;  // the deep tail's ticket counter
+        meta[2] = 0u;  // ... and its count of finished parts
     }
 }
 
@@ -1201,26 +1205,66 @@ __global__ __launch_bounds__(256) void ip_hole_layer_kernel(Chunk ch, const uint
 }
 
 // The layers beyond the ones the host launched (L0 .. meta[0], the deepest
-// layer the sort found), in ONE workgroup: layer after layer, each as the
-// kTailParts blocks of a kTailParts-block launch run one after another, a
-// workgroup barrier between layers (one CU: the layer's T / colour stores are
-// visible to every wave of the workgroup after it).  Nothing waits on another
-// workgroup, so no co-residency is assumed (other streams' kernels may hold
-// the CUs).  Exits at once when meta[0] < L0: the host launches every layer
-// of the recent calls at this shape (and every possible one when it has no
-// statistics yet), so the tail only sees a call deeper than those.
-constexpr unsigned kTailParts = 16;
+// layer the sort found), on a grid of kTailGrid workgroups: every layer is
+// cut into kTailParts parts (the partition of a kTailParts-block layer
+// launch), and the parts of all tail layers are tickets taken in order from
+// one counter (meta[1]).  A workgroup holding a part of layer L waits until
+// every part of layer L - 1 has finished (meta[2], the count of finished
+// parts: parts of layer L + 1 only finish after layer L has, so the first
+// (L - L0 + 1) * kTailParts finishes are exactly layers L0 .. L).
+// Deadlock-free without co-residency: tickets are taken in increasing order,
+// so every part a workgroup waits for was taken earlier -- by a running
+// workgroup, which finishes it (its own wait is on an earlier layer still;
+// layer L0 waits for nothing).  A workgroup that never starts holds no
+// ticket.  Results cross workgroups (and XCDs) through agent-scope
+// release / acquire fences around the counters.  The previous tail was one
+// workgroup doing the 16 parts of each layer one after another: a deep call
+// after a history of shallow ones at the same shape spent 600 ms there
+// (308 layers at 16 x 768x1024, tools/tail_cliff.py).
+// Exits at once when meta[0] < L0: the host launches every layer of the
+// recent calls at this shape (and every possible one when it has no
+// statistics yet), so the tail only runs for a call deeper than those.
+constexpr unsigned kTailParts = 64, kTailGrid = 64;
+constexpr unsigned kTailSpinBound = 1u << 26;  // sleeps before the wait gives up (seconds; never reached)
+
 __global__ __launch_bounds__(256) void ip_hole_tail_kernel(Chunk ch, const uint32_t *__restrict__ list,
                                                            const unsigned *__restrict__ hist,
-                                                           const unsigned *__restrict__ cursor, const unsigned *meta,
+                                                           const unsigned *__restrict__ cursor, unsigned *meta,
                                                            int nring, unsigned L0, int range, unsigned thin_cap) {
     __shared__ WavePatch patch[4];
+    __shared__ unsigned tk, bad;
     const unsigned lmax = meta[0];
-    if (threadIdx.x == 0 && lmax >= L0) atomicAdd(&g_ip_tail_layers, lmax - L0 + 1u);
-    for (unsigned L = L0; L <= lmax; ++L) {
-        for (unsigned bx = 0; bx < kTailParts; ++bx)
-            hole_layer_body(ch, list, hist, cursor, nring, L, range, thin_cap, patch, bx, kTailParts);
+    if (lmax < L0) return;  // uniform: no layer beyond the launched ones
+    if (threadIdx.x == 0 && blockIdx.x == 0) atomicAdd(&g_ip_tail_layers, lmax - L0 + 1u);
+    const unsigned total = (lmax - L0 + 1u) * kTailParts;
+    for (;;) {
+        if (threadIdx.x == 0) {
+            tk = atomicAdd(&meta[1], 1u);
+            bad = 0u;
+            const unsigned t = tk;
+            if (t < total && t >= kTailParts) {  // wait for layer L - 1: all of its parts are taken
+                const unsigned need = (t / kTailParts) * kTailParts;
+                unsigned spins = 0;
+                while (__hip_atomic_load(&meta[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+                    __builtin_amdgcn_s_sleep(4);
+                    if (++spins > kTailSpinBound) {
+                        atomicOr(&g_ip_fault, 8u);
+                        bad = 1u;
+                        break;
+                    }
+                }
+            }
+        }
         __syncthreads();
+        const unsigned t = tk, give_up = bad;
+        __syncthreads();  // tk / bad read by every thread before thread 0 rewrites them
+        if (t >= total || give_up) return;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the previous layers' T and colours
+        hole_layer_body(ch, list, hist, cursor, nring, L0 + t / kTailParts, range, thin_cap, patch, t % kTailParts,
+                        kTailParts);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __syncthreads();
+        if (threadIdx.x == 0) atomicAdd(&meta[2], 1u);
     }
 }
 
@@ -1442,7 +1486,7 @@ int ofd_inpaint_telea_f32(const float *img, const float *valid, const float *col
         hipLaunchKernelGGL(ip_negate_kernel, dim3(lag.valid ? std::max(16u, std::min(gdef, lag.ring / 256u + 4u)) : gdef),
                            dim3(256), 0, st, w.T, w.list, cursor, nring);
         // no statistics yet at this shape: every possible layer (an empty
-        // launch costs ~1.6 us), so the one-workgroup tail is left idle
+        // launch costs ~1.6 us), so the deep tail is left idle
         const int lmax_launch = g_launch_layers >= 0 ? std::min(g_launch_layers, int(H + W))
                                 : int(lag.valid ? std::min<unsigned>(lag.lmax + 2u, unsigned(H + W)) : unsigned(H + W));
         for (int L = 1; L <= lmax_launch; ++L) {
@@ -1458,7 +1502,7 @@ int ofd_inpaint_telea_f32(const float *img, const float *valid, const float *col
             hipLaunchKernelGGL(ip_hole_layer_kernel, dim3(g), dim3(256), 0, st, ch, w.list, hist, cursor, nring,
                                unsigned(L), r, thin_cap);
         }
-        hipLaunchKernelGGL(ip_hole_tail_kernel, dim3(1), dim3(256), 0, st, ch, w.list, hist, cursor, meta,
+        hipLaunchKernelGGL(ip_hole_tail_kernel, dim3(kTailGrid), dim3(256), 0, st, ch, w.list, hist, cursor, meta,
                            nring, unsigned(lmax_launch + 1), r, thin_cap);
         lagged_stats(nb, H, W, r).record(hist, meta, nbins, st);
     }

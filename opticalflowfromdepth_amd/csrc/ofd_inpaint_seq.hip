@@ -427,6 +427,7 @@ struct FmmLds {
     uint64_t keys2[kCap];  // LDS sort ping-pong
     uint32_t scr[40];
     uint32_t tmin, tmax, chg;
+    uint32_t chg3[3];  // the LDS distance sweeps' change flags (one barrier per sweep)
     uint32_t hk[kHash], hd[kHash], hc[kHash];  // distinct distance, its rank, its count
     uint32_t wc[kThreads / 64][kMaxD];         // per wave: keys of each rank in the current chunk
     uint32_t base[kMaxD], dv[kMaxD];
@@ -908,14 +909,17 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
                     Tl[i] = T_FAR;
                 }
             }
+            if (tid == 0) L.chg3[0] = 0u;
             __syncthreads();
+            // one barrier per sweep: sweep `it` flags changes in chg3[it % 3];
+            // chg3[(it + 1) % 3], last read right after barrier it - 2, is
+            // zeroed for the next sweep before this sweep's barrier
             for (uint32_t it = 0;; ++it) {
                 if (it > npush + 1) {
                     if (tid == 0) { m.meta[5] = 2u; atomicOr(&g_sq_fault, 4u); }
                     break;
                 }
-                if (tid == 0) L.chg = 0u;
-                __syncthreads();
+                if (tid == 0) L.chg3[(it + 1) % 3] = 0u;
 #pragma unroll
                 for (int u = 0; u < 2; ++u) {
                     const uint32_t i = tid + uint32_t(u) * kThreads;
@@ -932,13 +936,12 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
                                               fm_solve(tv[0], in[0], tv[3], in[3]), fm_solve(tv[2], in[2], tv[3], in[3]));
                         if (T != Tl[i]) {
                             Tl[i] = T;
-                            L.chg = 1u;
+                            L.chg3[it % 3] = 1u;
                         }
                     }
                 }
                 __syncthreads();
-                const uint32_t c = L.chg;
-                __syncthreads();
+                const uint32_t c = L.chg3[it % 3];
 #ifdef OFD_SQ_PROF
                 if (tid == 0) prof[pb + 6] += 1;
 #endif
@@ -1672,10 +1675,6 @@ __global__ __launch_bounds__(256, OFD_REC_MINW) void sq_record3_kernel(SqWs w) {
     }
 }
 
-#ifndef OFD_C3_PF  // probe knob: 0 = append at the level's end (base); 1 / 2 = append + record touch earlier
-#define OFD_C3_PF 0
-#endif
-
 struct C3Lds {
     uint32_t nnext[3];  // level l appends to nnext[l % 3]; reset two levels ahead (one barrier per level)
     uint64_t fr[2][kFrCap];
@@ -1776,13 +1775,7 @@ __global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, int C, int H, 
                     old[k] = atomicSub(&m.own[q], 1u);
                 }
             }
-            uint32_t pfv[8], pfw[8];  // OFD_C3_PF: record touches (values never used)
-#pragma unroll
-            for (int k = 0; k < 8; ++k) pfv[k] = pfw[k] = 0u;
-            // the holes whose last earlier neighbour this was join the next
-            // level; OFD_C3_PF > 0 (probe): appended earlier in the level, and
-            // each one's record lines touched then, so the next level's record
-            // loads hit L2 (the touch overlaps the rest of this level)
+            // the holes whose last earlier neighbour this was join the next level
             auto append_ready = [&]() {
 #pragma unroll
                 for (int k = 0; k < 8; ++k)
@@ -1794,11 +1787,6 @@ __global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, int C, int H, 
                             L.fr[cur ^ 1][f] = en;
                         else
                             gb[f] = en;
-                        if (OFD_C3_PF) {  // plain loads, consumed only at the round's end
-                            const uint32_t *rq = m.rec + size_t(old[k] >> 6) * kRecW;
-                            pfv[k] = rq[0];
-                            pfw[k] = rq[kRecW - 1];
-                        }
                     }
             };
             SQ_T(c1);
@@ -1858,7 +1846,6 @@ __global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, int C, int H, 
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (OFD_C3_PF == 1) append_ready();
             SQ_T(c2);
             // cv2's sums in its (k, l) order: chains gl and gl + 8 side by side
             // (independent accumulators; Ia chains add, Jx / Jy chains subtract)
@@ -1880,7 +1867,6 @@ __global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, int C, int H, 
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             SQ_T(c3);
-            if (OFD_C3_PF == 2) append_ready();
             if (act && gl < C) {
                 const float sum = __uint_as_float(mq.z);
                 const float Ia = L.res[g][3 * gl], Jx = L.res[g][3 * gl + 1], Jy = L.res[g][3 * gl + 2];
@@ -1890,15 +1876,10 @@ __global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, int C, int H, 
                 const unsigned u = sat_u8(sat);
                 shb[4 * (int64_t(i - 1) * W + (j - 1)) + gl] = uint8_t(u);
             }
-            // holes whose last earlier neighbour this was join the next level
-            if (OFD_C3_PF == 0) append_ready();
+            append_ready();
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (OFD_C3_PF) {
-#pragma unroll
-                for (int k = 0; k < 8; ++k) asm volatile("" ::"v"(pfv[k]), "v"(pfw[k]));
-            }
             SQ_T(c4);
             SQ_ACC(2, c0, c0a);
             SQ_ACC(6, c0a, c1);

@@ -298,13 +298,17 @@ def _check_file_vs_fill_fixture(z, pre, arr, kind=None):
             exact &= _digest(arr[c]) == str(dig[c])
         elif tolsum in z.files:
             # larger fixture: the strided sample within the tolerance, and the
-            # plane's sum and absolute sum within (pixels x tolerance)
+            # plane's sum and absolute sum within (pixels x tolerance).  The
+            # tolerance is the ego-flow module's bar (tests/test_ego.py): 8 ulp
+            # of the image's extent, as float32 flows near 255 px carry ulps of
+            # 1.5e-5 (1e-5 absolute stays the 32x40 images' bar)
+            atol = max(GEOMETRY_ATOL, 8 * float(np.spacing(np.float32(max(arr.shape[-2:]) - 1))))
             np.testing.assert_allclose(arr[c, ::sy, ::sx], z[pre + "/sample"][c].astype(arr.dtype), rtol=0,
-                                       atol=GEOMETRY_ATOL, err_msg=f"{pre} c{c} sample")
+                                       atol=atol, err_msg=f"{pre} c{c} sample")
             a64 = arr[c].astype(np.float64)
             ref_sum, ref_abs = (float(v) for v in z[tolsum])
-            assert abs(a64.sum() - ref_sum) <= a64.size * GEOMETRY_ATOL, (pre, c)
-            assert abs(np.abs(a64).sum() - ref_abs) <= a64.size * GEOMETRY_ATOL, (pre, c)
+            assert abs(a64.sum() - ref_sum) <= a64.size * atol, (pre, c)
+            assert abs(np.abs(a64).sum() - ref_abs) <= a64.size * atol, (pre, c)
             exact &= _digest(arr[c]) == str(dig[c])
         else:
             if _digest(arr[c]) != str(dig[c]):
