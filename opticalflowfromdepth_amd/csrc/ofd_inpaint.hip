@@ -1225,39 +1225,54 @@ __global__ __launch_bounds__(256) void ip_hole_layer_kernel(Chunk ch, const uint
 // recent calls at this shape (and every possible one when it has no
 // statistics yet), so the tail only runs for a call deeper than those.
 constexpr unsigned kTailParts = 64, kTailGrid = 64;
-constexpr unsigned kTailSpinBound = 1u << 26;  // sleeps before the wait gives up (seconds; never reached)
+constexpr unsigned kTailSpinBound = 1u << 20;  // polls before the wait gives up (~seconds; never reached)
 
 __global__ __launch_bounds__(256) void ip_hole_tail_kernel(Chunk ch, const uint32_t *__restrict__ list,
                                                            const unsigned *__restrict__ hist,
                                                            const unsigned *__restrict__ cursor, unsigned *meta,
                                                            int nring, unsigned L0, int range, unsigned thin_cap) {
     __shared__ WavePatch patch[4];
-    __shared__ unsigned tk, bad;
+    __shared__ unsigned tk[2];  // [ticket, gave up]
     const unsigned lmax = meta[0];
     if (lmax < L0) return;  // uniform: no layer beyond the launched ones
     if (threadIdx.x == 0 && blockIdx.x == 0) atomicAdd(&g_ip_tail_layers, lmax - L0 + 1u);
     const unsigned total = (lmax - L0 + 1u) * kTailParts;
+    const unsigned lane = threadIdx.x & 63u;
+    // Every branch below is uniform across the workgroup or across wave 0
+    // (values broadcast with shuffles / readfirstlane), so the loop's barriers
+    // are met the same number of times by every wave.
     for (;;) {
-        if (threadIdx.x == 0) {
-            tk = atomicAdd(&meta[1], 1u);
-            bad = 0u;
-            const unsigned t = tk;
-            if (t < total && t >= kTailParts) {  // wait for layer L - 1: all of its parts are taken
+        if (threadIdx.x < 64u) {  // wave 0 takes the next ticket and waits for the layer before it
+            unsigned t = 0u;
+            if (lane == 0u) t = atomicAdd(&meta[1], 1u);
+            t = __builtin_amdgcn_readfirstlane(t);
+            unsigned gave_up = 0u;
+            if (t < total && t >= kTailParts) {
                 const unsigned need = (t / kTailParts) * kTailParts;
-                unsigned spins = 0;
-                while (__hip_atomic_load(&meta[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
-                    __builtin_amdgcn_s_sleep(4);
-                    if (++spins > kTailSpinBound) {
-                        atomicOr(&g_ip_fault, 8u);
-                        bad = 1u;
+                for (unsigned spins = 0;; ++spins) {
+                    unsigned done = 0u;
+                    // polled with an atomic read-modify-write (+0), like every
+                    // other access to the counter
+                    if (lane == 0u) done = atomicAdd(&meta[2], 0u);
+                    done = __builtin_amdgcn_readfirstlane(done);
+                    if (done >= need) break;
+                    if (spins >= kTailSpinBound) {
+                        if (lane == 0u) atomicOr(&g_ip_fault, 8u);
+                        gave_up = 1u;
                         break;
                     }
+                    __builtin_amdgcn_s_sleep(4);
                 }
+            }
+            if (lane == 0u) {
+                tk[0] = t;
+                tk[1] = gave_up;
             }
         }
         __syncthreads();
-        const unsigned t = tk, give_up = bad;
-        __syncthreads();  // tk / bad read by every thread before thread 0 rewrites them
+        const unsigned t = __builtin_amdgcn_readfirstlane(tk[0]);
+        const unsigned give_up = __builtin_amdgcn_readfirstlane(tk[1]);
+        __syncthreads();  // every thread has read tk before wave 0 rewrites it
         if (t >= total || give_up) return;
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the previous layers' T and colours
         hole_layer_body(ch, list, hist, cursor, nring, L0 + t / kTailParts, range, thin_cap, patch, t % kTailParts,
