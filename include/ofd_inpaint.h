@@ -31,6 +31,9 @@
  *   ofd_inpaint_workspace_bytes, ofd_inpaint_seq_workspace_bytes
  *       no reference counterpart (cv2 allocates its fast-marching state per
  *       call); caller-owned scratch, no initialisation needed.
+ *   ofd_inpaint_seq_set_groups
+ *       no reference counterpart: how many stream-parallel groups the
+ *       sequential fill splits a batch into (results never depend on it).
  *   ofd_inpaint_set_schedule
  *       no reference counterpart: diagnostics / tests only (how many hole
  *       layers are launched one by one before the deep-tail
@@ -87,6 +90,16 @@ size_t ofd_inpaint_seq_workspace_bytes(int64_t B, int64_t H, int64_t W);
 int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float *collision, float *out,
                               int64_t B, int64_t C, int64_t H, int64_t W, int radius, void *workspace,
                               size_t workspace_bytes, void *stream);
+
+/* Sequential fill: split a batch into `groups` (1-4) groups of at least 2
+ * images, run on the caller's stream and up to three library helper streams
+ * (forked from and joined back into the caller's stream), each group in its
+ * own slice of the workspace -- one group's colour pass then overlaps
+ * another's fast march.  Applies when the whole batch fits the workspace as
+ * one chunk.  Results never depend on it.  groups < 0 only queries; the
+ * default comes from OFD_SEQ_GROUPS (else 1).  Process-wide;
+ * returns the previous setting. */
+int ofd_inpaint_seq_set_groups(int groups);
 
 /* Diagnostics: launch_layers >= 0 launches exactly that many hole layers one
  * by one (the deep-tail kernel does the rest); thin_cap >= 0 sets the layer

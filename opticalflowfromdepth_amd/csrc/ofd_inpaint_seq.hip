@@ -1923,6 +1923,54 @@ __global__ __launch_bounds__(256) void sq_unpack_kernel(SqWs w, float *__restric
     for (int c = 0; c < C; ++c) ob[int64_t(c) * HW] = float((v >> (8 * c)) & 0xFFu);
 }
 
+
+// Helper streams and events of the grouped sequential fill (seq_groups), one
+// set per process (created on first use on the current device).
+struct SeqHelpers {
+    bool ok = false;
+    hipStream_t stream[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t fork = nullptr, join[3] = {nullptr, nullptr, nullptr};
+};
+
+SeqHelpers &seq_helpers() {
+    static SeqHelpers h = [] {
+        SeqHelpers v;
+        bool ok = hipEventCreateWithFlags(&v.fork, hipEventDisableTiming) == hipSuccess;
+        for (int k = 0; k < 3 && ok; ++k)
+            ok = hipStreamCreateWithFlags(&v.stream[k], hipStreamNonBlocking) == hipSuccess &&
+                 hipEventCreateWithFlags(&v.join[k], hipEventDisableTiming) == hipSuccess;
+        v.ok = ok;
+        return v;
+    }();
+    return h;
+}
+
+// Groups of the batch (OFD_SEQ_GROUPS, default 1; at most 4): only when
+// every group of ceil(B / groups) images fits its own 256-aligned slice of
+// the workspace in one chunk, and each group holds at least 2 images.
+#ifndef OFD_SEQ_GROUPS_DEFAULT
+#define OFD_SEQ_GROUPS_DEFAULT 1
+#endif
+int g_seq_groups = -1;  // ofd_inpaint_seq_set_groups; -1 = not set (OFD_SEQ_GROUPS, else the default)
+int seq_groups_setting() {
+    if (g_seq_groups < 0) {
+        const char *e = getenv("OFD_SEQ_GROUPS");
+        const int v = e ? atoi(e) : OFD_SEQ_GROUPS_DEFAULT;
+        g_seq_groups = v < 1 ? 1 : (v > 4 ? 4 : v);
+    }
+    return g_seq_groups;
+}
+
+int seq_groups(int64_t B, int64_t G, size_t pi, size_t avail) {
+    int ng = seq_groups_setting();
+    while (ng > 1) {
+        const int64_t per = (B + ng - 1) / ng;
+        if (per >= 2 && G >= B && size_t(ng) * align256(size_t(per) * pi) <= avail) break;
+        --ng;
+    }
+    return ng;
+}
+
 }  // namespace
 
 unsigned ofd_sq_fault_read(int reset) {
@@ -1936,6 +1984,12 @@ unsigned ofd_sq_fault_read(int reset) {
 }
 
 extern "C" {
+
+int ofd_inpaint_seq_set_groups(int groups) {
+    const int prev = seq_groups_setting();
+    if (groups >= 1) g_seq_groups = groups > 4 ? 4 : groups;
+    return prev;
+}
 
 size_t ofd_inpaint_seq_workspace_bytes(int64_t B, int64_t H, int64_t W) {
     if (B <= 0 || H <= 0 || W <= 0) return 0;
@@ -1962,7 +2016,6 @@ int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float 
     int64_t G = int64_t((workspace_bytes - fixed) / pi);
     if (G > B) G = B;
     hipStream_t st = static_cast<hipStream_t>(stream);
-    const SqWs w = carve(workspace, G, H, W);
     // radius 3 with up to 3 channels (utils.inpaint's RGB call): the record
     // path; OFD_SEQ_COLOUR=g16 selects the one-pass colour kernel (A/B)
     static const bool force_g16 = [] {
@@ -1975,40 +2028,69 @@ int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float 
         return e ? atof(e) : 0.7;
     }();
     const double bscale = (H + W < 8000 && wide > 0.0 && wide <= 0.7) ? 1.0 / wide : 2.0;
-    for (int64_t b0 = 0; b0 < B; b0 += G) {
-        const int64_t nb = B - b0 < G ? B - b0 : G;
+    // one chunk of nb images (workspace w) on stream s
+    auto run_chunk = [&](const SqWs &w, int64_t b0, int64_t nb, hipStream_t s) {
         hipLaunchKernelGGL(sq_prep_tile_kernel, dim3(unsigned((W + 63) / 64), unsigned((H + 15) / 16), unsigned(nb)),
-                           dim3(256), 0, st, img, valid, collision, out, w, int(C), int(H), int(W), b0, rec3 ? 1 : 0);
+                           dim3(256), 0, s, img, valid, collision, out, w, int(C), int(H), int(W), b0, rec3 ? 1 : 0);
         if (r <= kInitR)
             hipLaunchKernelGGL(sq_init_tile_kernel,
                                dim3(unsigned((w.ew + kInitTW - 1) / kInitTW), unsigned((w.eh + kInitTH - 1) / kInitTH),
                                     unsigned(nb)),
-                               dim3(256), 0, st, w, r);
+                               dim3(256), 0, s, w, r);
         else
-            hipLaunchKernelGGL(sq_init_kernel, dim3(unsigned((w.eh + 3) / 4), unsigned(nb)), dim3(256), 0, st, w, r);
-        hipLaunchKernelGGL(sq_band_scan_kernel, dim3(unsigned(nb)), dim3(kThreads), 0, st, w);
-        hipLaunchKernelGGL(sq_band_write_kernel, dim3(unsigned((w.eh + 3) / 4), unsigned(nb)), dim3(256), 0, st, w);
-        hipLaunchKernelGGL(sq_fmm_kernel, dim3(unsigned(nb), 2u), dim3(kThreads), 0, st, w, bscale);
+            hipLaunchKernelGGL(sq_init_kernel, dim3(unsigned((w.eh + 3) / 4), unsigned(nb)), dim3(256), 0, s, w, r);
+        hipLaunchKernelGGL(sq_band_scan_kernel, dim3(unsigned(nb)), dim3(kThreads), 0, s, w);
+        hipLaunchKernelGGL(sq_band_write_kernel, dim3(unsigned((w.eh + 3) / 4), unsigned(nb)), dim3(256), 0, s, w);
+        hipLaunchKernelGGL(sq_fmm_kernel, dim3(unsigned(nb), 2u), dim3(kThreads), 0, s, w, bscale);
 #ifdef OFD_BUCKET_TRACE
-        continue;  // probe: keep the record area (the inner march's bucket trace) for the host
+        return;  // probe: keep the record area (the inner march's bucket trace) for the host
 #endif
         if (rec3) {
             hipLaunchKernelGGL(sq_record3_kernel,
                                dim3(unsigned((w.ew + 63) / 64), unsigned((w.eh + kRecTH - 1) / kRecTH), unsigned(nb)),
-                               dim3(256), 0, st, w);
-            hipLaunchKernelGGL(sq_colour3_kernel, dim3(unsigned(nb)), dim3(1024), 0, st, w, int(C), int(H), int(W));
-            hipLaunchKernelGGL(sq_unpack_kernel, dim3(unsigned((H * W + 255) / 256), unsigned(nb)), dim3(256), 0, st, w,
+                               dim3(256), 0, s, w);
+            hipLaunchKernelGGL(sq_colour3_kernel, dim3(unsigned(nb)), dim3(1024), 0, s, w, int(C), int(H), int(W));
+            hipLaunchKernelGGL(sq_unpack_kernel, dim3(unsigned((H * W + 255) / 256), unsigned(nb)), dim3(256), 0, s, w,
                                out, int(C), int64_t(H * W), b0);
-            continue;
+            return;
         }
         hipLaunchKernelGGL(sq_count_kernel, dim3(unsigned((w.ew + 63) / 64), unsigned((w.eh + 3) / 4), unsigned(nb)),
-                           dim3(256), 0, st, w, r);
+                           dim3(256), 0, s, w, r);
         if (r == 3)
-            hipLaunchKernelGGL(sq_colour_g16_kernel, dim3(unsigned(nb)), dim3(kG16Threads), 0, st, w, out, int(C), int(H),
+            hipLaunchKernelGGL(sq_colour_g16_kernel, dim3(unsigned(nb)), dim3(kG16Threads), 0, s, w, out, int(C), int(H),
                                int(W), b0);
         else
-            hipLaunchKernelGGL(sq_colour_kernel, dim3(unsigned(nb)), dim3(kColThreads), 0, st, w, out, int(C), int(H),
+            hipLaunchKernelGGL(sq_colour_kernel, dim3(unsigned(nb)), dim3(kColThreads), 0, s, w, out, int(C), int(H),
                                int(W), b0, r);
+    };
+    // Groups: the batch split over the caller's stream and up to three
+    // helper streams, each group's chunk in its own slice of the workspace.
+    // An image's chain (FMM, then its Kahn levels) is serial and takes one or
+    // two CUs, so a single chunk costs max FMM + max COLOUR over all its
+    // images; groups overlap one group's colour pass with another's march.
+    const int ng = seq_groups(B, G, pi, workspace_bytes - fixed);
+    if (ng <= 1) {
+        const SqWs w = carve(workspace, G, H, W);
+        for (int64_t b0 = 0; b0 < B; b0 += G) run_chunk(w, b0, B - b0 < G ? B - b0 : G, st);
+    } else {
+        SeqHelpers &hp = seq_helpers();
+        if (!hp.ok) return OFD_FW_EWORKSPACE;
+        hipError_t e = hipEventRecord(hp.fork, st);
+        const int64_t per = (B + ng - 1) / ng;
+        const size_t stride = align256(size_t(per) * pi);
+        for (int k = 0; k < ng && e == hipSuccess; ++k) {
+            const int64_t b0 = int64_t(k) * per, nb = std::min<int64_t>(per, B - b0);
+            if (nb <= 0) break;
+            hipStream_t s = k == 0 ? st : hp.stream[k - 1];
+            if (k > 0) e = hipStreamWaitEvent(s, hp.fork, 0);
+            if (e != hipSuccess) break;
+            run_chunk(carve(static_cast<char *>(workspace) + size_t(k) * stride, nb, H, W), b0, nb, s);
+            if (k > 0) {
+                e = hipEventRecord(hp.join[k - 1], s);
+                if (e == hipSuccess) e = hipStreamWaitEvent(st, hp.join[k - 1], 0);
+            }
+        }
+        if (e != hipSuccess) return int(e);
     }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? OFD_FW_OK : int(e);

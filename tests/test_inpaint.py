@@ -459,3 +459,32 @@ def test_inpaint_sequential_wide_image_half_unit_buckets():
     got = ops.inpaint(torch.from_numpy(img * v).to(dev), torch.from_numpy(v).to(dev), torch.from_numpy(c).to(dev),
                       order="sequential").cpu().numpy()
     assert np.array_equal(got, oracle.inpaint(img * v, v, c, 3, layered=False))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("groups", [2, 4])
+def test_inpaint_sequential_stream_groups(groups):
+    """ofd_inpaint_seq_set_groups: the batch split over the caller's stream and
+    library helper streams (each group in its own workspace slice, forked from
+    and joined back into the caller's stream) gives the one-stream result bit
+    for bit, and the oracle's; the caller's stream sees the whole fill."""
+    from opticalflowfromdepth_amd import _native, forward_warp_flow, ops, synth
+    lib = _native.lib()
+    dev = torch.device("cuda:0")
+    seeds = [12345, 12346, 12377, 12378, 12401, 12402, 12433, 12434]
+    obj, flow, depth = synth.stage_one_batch(seeds, 384, 512, dev)
+    out, valid, coll = forward_warp_flow(obj, flow, depth)
+    rgb = (out[:, 0:3] * valid).contiguous()
+    prev = lib.ofd_inpaint_seq_set_groups(1)
+    try:
+        one = ops.inpaint(rgb, valid, coll, order="sequential")
+        lib.ofd_inpaint_seq_set_groups(groups)
+        side = torch.cuda.Stream()
+        with torch.cuda.stream(side):
+            got = ops.inpaint(rgb, valid, coll, order="sequential")
+            got_host = got.cpu().numpy()  # synchronises the caller's (side) stream only
+    finally:
+        lib.ofd_inpaint_seq_set_groups(prev)
+    assert np.array_equal(got_host, one.cpu().numpy())
+    exp = oracle.inpaint(rgb.cpu().numpy(), valid.cpu().numpy(), coll.cpu().numpy(), 3, layered=False)
+    assert np.array_equal(got_host, exp)
