@@ -15,6 +15,6 @@ for round in $(seq "$ROUNDS"); do
       *) lib="$PWD/opticalflowfromdepth_amd/_build/libofd_fw_$v.so" ;;
     esac
     env "$envv" OFD_FW_LIB=$lib timeout -k 10 120 python tools/seq_time.py "$B" > /tmp/ab_seq.txt 2>&1 || exit 1
-    echo "$v $(grep '^sequential' /tmp/ab_seq.txt)"
+    echo "$v $(grep "^${PHASE:-sequential}" /tmp/ab_seq.txt)"
   done
 done
