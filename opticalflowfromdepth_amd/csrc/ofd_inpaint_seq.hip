@@ -53,6 +53,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <mutex>
+
 #include "ofd_fw.h"
 #include "ofd_inpaint.h"
 
@@ -1927,21 +1929,22 @@ __global__ __launch_bounds__(256) void sq_unpack_kernel(SqWs w, float *__restric
 // Helper streams and events of the grouped sequential fill (seq_groups), one
 // set per process (created on first use on the current device).
 struct SeqHelpers {
+    std::mutex mu;
     bool ok = false;
     hipStream_t stream[3] = {nullptr, nullptr, nullptr};
     hipEvent_t fork = nullptr, join[3] = {nullptr, nullptr, nullptr};
 };
 
 SeqHelpers &seq_helpers() {
-    static SeqHelpers h = [] {
-        SeqHelpers v;
-        bool ok = hipEventCreateWithFlags(&v.fork, hipEventDisableTiming) == hipSuccess;
+    static SeqHelpers h;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        bool ok = hipEventCreateWithFlags(&h.fork, hipEventDisableTiming) == hipSuccess;
         for (int k = 0; k < 3 && ok; ++k)
-            ok = hipStreamCreateWithFlags(&v.stream[k], hipStreamNonBlocking) == hipSuccess &&
-                 hipEventCreateWithFlags(&v.join[k], hipEventDisableTiming) == hipSuccess;
-        v.ok = ok;
-        return v;
-    }();
+            ok = hipStreamCreateWithFlags(&h.stream[k], hipStreamNonBlocking) == hipSuccess &&
+                 hipEventCreateWithFlags(&h.join[k], hipEventDisableTiming) == hipSuccess;
+        h.ok = ok;
+    });
     return h;
 }
 
@@ -2075,6 +2078,9 @@ int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float 
     } else {
         SeqHelpers &hp = seq_helpers();
         if (!hp.ok) return OFD_FW_EWORKSPACE;
+        // one caller at a time enqueues on the shared helper streams: each
+        // event's record / wait pair must not interleave with another's
+        std::lock_guard<std::mutex> lk(hp.mu);
         hipError_t e = hipEventRecord(hp.fork, st);
         const int64_t per = (B + ng - 1) / ng;
         const size_t stride = align256(size_t(per) * pi);
