@@ -488,3 +488,41 @@ def test_inpaint_sequential_stream_groups(groups):
     assert np.array_equal(got_host, one.cpu().numpy())
     exp = oracle.inpaint(rgb.cpu().numpy(), valid.cpu().numpy(), coll.cpu().numpy(), 3, layered=False)
     assert np.array_equal(got_host, exp)
+
+
+@pytest.mark.gpu
+def test_inpaint_sequential_stream_groups_concurrent_callers():
+    """Two host threads fill different batches with stream groups on their own
+    streams at once: the library's helper streams are shared, and each call's
+    fork / join stays its own (results equal the one-stream fills)."""
+    import threading
+    from opticalflowfromdepth_amd import _native, forward_warp_flow, ops, synth
+    lib = _native.lib()
+    dev = torch.device("cuda:0")
+    batches = []
+    for seeds in ([12345, 12346, 12377, 12378], [12401, 12402, 12433, 12434]):
+        obj, flow, depth = synth.stage_one_batch(seeds, 256, 320, dev)
+        out, valid, coll = forward_warp_flow(obj, flow, depth)
+        batches.append(((out[:, 0:3] * valid).contiguous(), valid, coll))
+    prev = lib.ofd_inpaint_seq_set_groups(1)
+    try:
+        ref = [ops.inpaint(*x, order="sequential").cpu().numpy() for x in batches]
+        lib.ofd_inpaint_seq_set_groups(2)
+        got = [None, None]
+
+        def run(i):
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                for _ in range(3):
+                    r = ops.inpaint(*batches[i], order="sequential")
+                got[i] = r.cpu().numpy()
+
+        th = [threading.Thread(target=run, args=(i,)) for i in range(2)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+    finally:
+        lib.ofd_inpaint_seq_set_groups(prev)
+    for i in range(2):
+        assert np.array_equal(got[i], ref[i])
