@@ -1080,6 +1080,10 @@ __global__ __launch_bounds__(kThreads) void sq_fmm_kernel(SqWs w, double bscale)
     const uint32_t nb = m.meta[0];
     uint32_t nbk = 0;
     uint64_t prof[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    // each march's duration on the constant-rate wall clock (meta[24] outer,
+    // meta[25] inner; tools/seq_time.py) -- those words hold the large-bucket
+    // probe clocks in OFD_SQ_PROF builds instead
+    const uint64_t w0 = threadIdx.x == 0 ? wall_clock64() : 0;
     if (blockIdx.y == 0) {
         const Img o = outer_view(m);
         const uint32_t no = fmm_pass<false>(o, m.sO, nb, L, nbk, prof, bscale);
@@ -1087,11 +1091,19 @@ __global__ __launch_bounds__(kThreads) void sq_fmm_kernel(SqWs w, double bscale)
             const uint32_t p = o.logp[i];
             m.t[p] = -m.t[p];
         }
-        if (threadIdx.x == 0) atomicAdd(&m.meta[4], nbk);
+        if (threadIdx.x == 0) {
+            atomicAdd(&m.meta[4], nbk);
+#ifndef OFD_SQ_PROF
+            m.meta[24] = uint32_t(wall_clock64() - w0);
+#endif
+        }
         return;
     }
     const uint32_t ni = fmm_pass<true>(m, m.sI, nb, L, nbk, prof, bscale);
     if (threadIdx.x == 0) {
+#ifndef OFD_SQ_PROF
+        m.meta[25] = uint32_t(wall_clock64() - w0);
+#endif
         m.meta[1] = ni - nb;
         m.meta[2] = 0u;
         atomicAdd(&m.meta[4], nbk);

@@ -46,6 +46,13 @@ def main():
     ws = ops._ip_workspaces[key]
     m = seq_meta(ws, B, 768, 1024)
     print("meta columns: band, pushes, level0, levels, buckets, error, colour3 rounds, levels <= 64 holes")
+    if not m[:, 8:24].any():  # non-probe build: each march's wall-clock duration (100 MHz ticks)
+        o, i = m[:, 24].astype(np.float64) / 100.0, m[:, 25].astype(np.float64) / 100.0
+        print(f"marches (us, 100 MHz wall clock): outer max {o.max():.0f} (image {int(o.argmax())}), "
+              f"inner max {i.max():.0f} (image {int(i.argmax())}); images whose outer march is the longer: "
+              f"{int((o > i).sum())} of {len(o)}")
+        for k in np.argsort(-np.maximum(o, i))[:6]:
+            print(f"  image {int(k)}: outer {o[k]:.0f} us, inner {i[k]:.0f} us, levels {int(m[k, 3])}")
     for k in np.argsort(-m[:, 3])[:8]:
         print(k, m[k, :8].tolist())
     eh, ew = 770, 1026
