@@ -87,6 +87,25 @@ def test_disparity_rows_switch():
     lib.ofd_fw_set_disparity_rows(cur)
 
 
+def test_schedule_setters_are_host_state():
+    """The persistent-SPLAT threshold and the sequential fill's stream groups
+    are process-wide host settings: a negative value queries, a valid one
+    sets and returns the previous (groups clamp to 1..4)."""
+    from opticalflowfromdepth_amd import _native
+    lib = _native.lib()
+    cur = lib.ofd_fw_set_persist_min(-1)
+    assert cur >= 0
+    assert lib.ofd_fw_set_persist_min(7) == cur
+    assert lib.ofd_fw_set_persist_min(-1) == 7
+    lib.ofd_fw_set_persist_min(cur)
+    g = lib.ofd_inpaint_seq_set_groups(-1)
+    assert 1 <= g <= 4
+    assert lib.ofd_inpaint_seq_set_groups(9) == g
+    assert lib.ofd_inpaint_seq_set_groups(2) == 4
+    assert lib.ofd_inpaint_seq_set_groups(-1) == 2
+    lib.ofd_inpaint_seq_set_groups(g)
+
+
 def test_argument_errors_without_gpu():
     """Validation happens before any HIP call, so it is testable on CPU."""
     from opticalflowfromdepth_amd import _native
