@@ -138,6 +138,26 @@ def test_gpu_npz_writer_files_load_back(cuda_device, tmp_path):
 
 
 @pytest.mark.gpu
+def test_gpu_npz_writer_reports_a_failed_write(cuda_device, tmp_path):
+    """save_batch returns at once (the deflate, the copies and the writes run
+    behind it); a write that fails -- here a path under a regular file -- is
+    raised by flush / close, and the writer's other files are still written."""
+    from opticalflowfromdepth_amd.npz_gpu import GpuNpzWriter
+    x = torch.randn(3, 8, 32, 40, device=cuda_device)
+    blocker = tmp_path / "not_a_dir"
+    blocker.write_bytes(b"")
+    ok = [str(tmp_path / "a.npz"), str(tmp_path / "b.npz")]
+    w = GpuNpzWriter(workers=2)
+    w.save_batch(ok + [str(blocker / "c.npz")], x)
+    with pytest.raises(OSError):
+        w.flush()
+    w.close()
+    xs = x.cpu().numpy()
+    for i, p in enumerate(ok):
+        assert np.array_equal(np.load(p)["img_depth_flow"], xs[i])
+
+
+@pytest.mark.gpu
 def test_pipeline_files_with_gpu_writer_equal_zlib_writer(cuda_device, tmp_path):
     """run_batch writing its 121 files per image through the GPU writer: every
     array np.load-equal to the same run through the zlib NpzWriter."""
