@@ -109,6 +109,16 @@ int ofd_fw_set_disparity_rows(int on);
  * previous setting.  Process-wide, not thread-safe against concurrent calls. */
 int ofd_fw_set_persist_min(int tiles_per_slot);
 
+/* Packed targets in the default TILE engine: BIN writes each source's target
+ * as 16 bits relative to its source block's tile box and SPLAT re-reads those
+ * 2 bytes instead of the coordinate planes (for FW on a flow / safe
+ * coordinates and ofd_fw_warp_flow_cat; the fused disparity / ego-motion
+ * warps read only the depth anyway).  on = 1 (default) / 0 for subsequent
+ * calls (also OFD_FW_PACK=0); any other value only queries.  Results are
+ * identical.  Returns the previous setting.  Process-wide, not thread-safe
+ * against concurrent calls. */
+int ofd_fw_set_pack(int on);
+
 /* Benchmark hook: when non-NULL, the given hipEvent_t's are recorded on the
  * launch stream right before the first and right after the last launch of
  * each subsequent f32 call's dominant kernel: SPLAT (TILE engine), RESOLVE

@@ -31,9 +31,10 @@
  *   ofd_inpaint_workspace_bytes, ofd_inpaint_seq_workspace_bytes
  *       no reference counterpart (cv2 allocates its fast-marching state per
  *       call); caller-owned scratch, no initialisation needed.
- *   ofd_inpaint_seq_set_groups
+ *   ofd_inpaint_seq_set_groups, ofd_inpaint_seq_helper_device
  *       no reference counterpart: how many stream-parallel groups the
- *       sequential fill splits a batch into (results never depend on it).
+ *       sequential fill splits a batch into (results never depend on it),
+ *       and the device whose helper streams a call would use.
  *   ofd_inpaint_set_schedule
  *       no reference counterpart: diagnostics / tests only (how many hole
  *       layers are launched one by one before the deep-tail
@@ -100,6 +101,11 @@ int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float 
  * default comes from OFD_SEQ_GROUPS (else 1).  Process-wide;
  * returns the previous setting. */
 int ofd_inpaint_seq_set_groups(int groups);
+
+/* The device whose helper streams a grouped sequential fill on `stream`
+ * would use: the stream's own device (helpers are kept per device and
+ * created there on first use), or -1 if it cannot be told. */
+int ofd_inpaint_seq_helper_device(void *stream);
 
 /* Diagnostics: launch_layers >= 0 launches exactly that many hole layers one
  * by one (the deep-tail kernel does the rest); thin_cap >= 0 sets the layer

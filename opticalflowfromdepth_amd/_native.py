@@ -35,6 +35,7 @@ SIGNATURES = {
     "ofd_fw_set_engine": ([ctypes.c_int], ctypes.c_int),
     "ofd_fw_set_disparity_rows": ([ctypes.c_int], ctypes.c_int),
     "ofd_fw_set_persist_min": ([ctypes.c_int], ctypes.c_int),
+    "ofd_fw_set_pack": ([ctypes.c_int], ctypes.c_int),
     "ofd_fw_set_profile_events": ([_P, _P], ctypes.c_int),
     "ofd_fw_workspace_bytes": ([_I64, _I64, _I64, ctypes.c_int], _SZ),
     "ofd_fw_workspace_init": ([_P, _SZ, _P], ctypes.c_int),
@@ -59,6 +60,7 @@ SIGNATURES = {
     "ofd_inpaint_faults": ([ctypes.c_int], ctypes.c_int),
     "ofd_inpaint_tail_layers": ([ctypes.c_int], ctypes.c_int),
     "ofd_inpaint_seq_set_groups": ([ctypes.c_int], ctypes.c_int),
+    "ofd_inpaint_seq_helper_device": ([ctypes.c_void_p], ctypes.c_int),
     "ofd_deflate_bound": ([_I64], _SZ),
     "ofd_deflate_workspace_bytes": ([_I64, _I64], _SZ),
     "ofd_deflate_batch": ([_P, _I64, _I64, _P, _P, _P, _P, _SZ, _P], ctypes.c_int),

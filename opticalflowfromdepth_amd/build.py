@@ -35,13 +35,25 @@ def hipcc() -> str:
 ID_FILE = OUT + ".id"
 
 
+def compile_flags() -> list:
+    """hipcc's flags for the library, without the compiler path, the output
+    name and the build id.  -ffp-contract=off: the hole-fill's float / double
+    sequence must be the oracle's bit for bit (the warp has no contractible
+    arithmetic)."""
+    return [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-Wall",
+            "-I", "include"]
+
+
 def source_hash() -> str:
     """The build id: first 16 hex digits of the SHA-256 over every source
-    the library is compiled from (name and bytes, in a fixed order).  The
-    library embeds it (ofd_fw_build_id) and a sidecar file records it, so a
-    binary can be tied to the sources -- i.e. the commit -- it came from."""
+    the library is compiled from (name and bytes, in a fixed order) and the
+    compile flags (target arch included), so a flag or arch change yields a
+    new id and a rebuild.  The library embeds it (ofd_fw_build_id) and a
+    sidecar file records it, so a binary can be tied to the sources -- i.e.
+    the commit -- it came from."""
     import hashlib
     h = hashlib.sha256()
+    h.update(" ".join(compile_flags()).encode() + b"\0")
     for p in SRCS + HDRS:
         h.update(os.path.relpath(p, REPO).encode() + b"\0")
         with open(p, "rb") as f:
@@ -70,11 +82,9 @@ def build_native(force: bool = False, verbose: bool = False) -> str:
         return OUT
     os.makedirs(OUT_DIR, exist_ok=True)
     tmp = OUT + f".tmp{os.getpid()}"
-    # -ffp-contract=off: the hole-fill's float / double sequence must be the
-    # oracle's bit for bit (the warp has no contractible arithmetic)
     bid = source_hash()
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
-           "-Wall", f'-DOFD_BUILD_ID="{bid}"', "-I", os.path.join(REPO, "include"), "-o", tmp] + SRCS
+    flags = [os.path.join(REPO, "include") if f == "include" else f for f in compile_flags()]
+    cmd = [hipcc()] + flags + [f'-DOFD_BUILD_ID="{bid}"', "-o", tmp] + SRCS
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

@@ -172,6 +172,12 @@ __device__ __forceinline__ void load4(const T *__restrict__ q, T v[4], int n) {
 // and that generate no obj channels.
 #define KEY_DEPTH_FROM_PLANE                                                                            \
     static constexpr int kGen = 0, kGenGT = 0;                                                        \
+    static constexpr bool kPackable = true;                                                           \
+    template <bool kVec>                                                                              \
+    __device__ __forceinline__ void load4k(int64_t b, int64_t p, float dk[4], int n,                  \
+                                           const float *depth) const {                                \
+        ::load4<kVec>(depth + b * HW + p, dk, n);                                                     \
+    }                                                                                                 \
     template <bool kVec>                                                                              \
     __device__ __forceinline__ void load4d(int64_t b, int64_t p, V x[4], V y[4], float dk[4], int n,  \
                                            const float *depth) const {                                \
@@ -240,6 +246,7 @@ template <typename D>
 struct DisparityCoords {
     using V = D;
     static constexpr int kGen = 3, kGenGT = 8;
+    static constexpr bool kPackable = false;  // SPLAT reads only the depth already
     const D *depth;
     const float *s;  // [B] per-image scale
     int64_t HW;
@@ -374,6 +381,7 @@ struct EgoCoords {
     // sources has been issued, which keeps SPLAT's loads in flight together.
     using V = D;
     static constexpr int kGen = 3, kGenGT = 4;
+    static constexpr bool kPackable = false;  // BIN bounds targets approximately; SPLAT reads only the depth
     const D *depth;
     const float *P;  // [B][3][4] float32 (K @ T)[:3]
     EgoCam cam;
@@ -460,9 +468,17 @@ template <typename F, typename D>
 struct FlowCatCoords {
     using V = F;
     static constexpr int kGen = 3, kGenGT = 8;
+    static constexpr bool kPackable = true;
     const F *flow;   // [B,2,H,W]
     const D *depth;  // [B,1,H,W]
     int64_t HW;
+    template <bool kVec>
+    __device__ __forceinline__ void load4k(int64_t b, int64_t p, float dk[4], int n, const float *) const {
+        D d[4];
+        ::load4<kVec>(depth + b * HW + p, d, n);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dk[e] = float(d[e]);
+    }
     __device__ __forceinline__ void load(int64_t b, int64_t p, V &x, V &y) const {
         const F *f = flow + b * 2 * HW + p;
         x = f[0];
@@ -607,7 +623,8 @@ inline size_t per_image_bytes(int64_t H, int64_t W) {
 
 struct Ws {  // views of one chunk's workspace (G images)
     unsigned long long *keys;  // [G][HW]      KEY_UNTOUCHED between calls
-    unsigned int *winner;      // [G][HW]      scratch: winning source index, ~0 = none
+    unsigned int *winner;      // [G][HW]      scratch: winning source index, ~0 = none (split engine)
+    unsigned short *code;      // [G][HW]      scratch, aliases winner's first half: packed targets (fused engine)
     unsigned int *flag;        // [G][ntiles]  0 = merge key slab, ~0 = clean
     ushort4 *segrec;           // [G][nseg]    scratch: target tile box (t0x,t1x,t0y,t1y) of a segment
     ushort4 *blkrec;           // [G][nsb]     scratch: same per source block
@@ -620,6 +637,7 @@ inline Ws carve(void *ws, int64_t G, int64_t HW, const TileGeom &g) {
     w.keys = reinterpret_cast<unsigned long long *>(p);
     p += align16(size_t(G) * size_t(HW) * 8);
     w.winner = reinterpret_cast<unsigned int *>(p);
+    w.code = reinterpret_cast<unsigned short *>(p);  // never used by the same call as winner
     p += align16(size_t(G) * size_t(HW) * 4);
     w.flag = reinterpret_cast<unsigned int *>(p);
     p += align16(size_t(G) * g.ntiles * 4);
@@ -699,7 +717,24 @@ __device__ __forceinline__ unsigned quad_min_pk16(unsigned v) {
 // instruction, and the segment box is a 3-step xor reduction over the quads
 // (8 readlanes and 9 single-lane stores before: 98 -> 72 us per 64 images,
 // and 76 -> 56 VGPRs, i.e. 8 waves per SIMD).
-template <typename Coords>
+// Packed target (kPack; coordinate sources with exact BIN targets): BIN
+// writes every source's target as 16 bits relative to its block's box --
+// (tile index within the box, <= 11) << 12 | offset inside that tile (ly * TW
+// + lx) -- so SPLAT re-reads 2 bytes per source instead of the coordinate
+// planes (8 bytes for a float32 flow) and needs no target arithmetic: a
+// source lands in SPLAT's tile iff its code's high nibble is the tile's index
+// in the block's box, and the low 12 bits are its z-buffer slot.  0xFFFF:
+// dropped source (NaN coordinate; no box holds 15 tiles).
+static_assert(TW * TH <= 4096 && MAX_TILES_PER_BLOCK <= 15, "packed target: 12-bit tile offset, 4-bit tile index");
+constexpr unsigned short CODE_NONE = 0xFFFF;
+
+__device__ __forceinline__ unsigned short pack_target(int tx, int ty, int t0x, int t0y, int bw) {
+    if (tx < 0) return CODE_NONE;
+    const int k = (ty / TH - t0y) * bw + (tx / TW - t0x);
+    return (unsigned short)((unsigned(k) << 12) | unsigned((ty % TH) * TW + tx % TW));
+}
+
+template <typename Coords, bool kPack = false, bool kVec = false>
 __device__ __forceinline__ void bin_segment(const Coords &co, const float *__restrict__ depth, const ChunkArgs &a,
                                                int H, int W, int64_t HW, const TileGeom &g, int64_t sgg,
                                                const typename Coords::V (&x)[2][4], const typename Coords::V (&y)[2][4]) {
@@ -745,6 +780,34 @@ __device__ __forceinline__ void bin_segment(const Coords &co, const float *__res
         ws.blkrec[int64_t(bl) * g.nsb + int64_t(sby) * g.nsbx + sbx] =
             boxed ? make_ushort4((unsigned short)t0x, (unsigned short)t1x, (unsigned short)t0y, (unsigned short)t1y)
                   : empty_box();
+    if constexpr (kPack) {
+        // this lane's 2 x 4 sources: one 8-byte store per row (kVec); the
+        // exact targets are recomputed (keeping 8 of them live through the
+        // box reduction would spill at BIN's 64-VGPR budget)
+        const int bw = t1x - t0x + 1;
+        unsigned short *cb = ws.code + int64_t(bl) * HW;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int j = jh + 2 * q;
+            if (j >= H || i0 >= W) continue;
+            unsigned short c[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                int tx = -1, ty = -1;
+                if (boxed && i0 + e < W) co.target(b, i0 + e, j, x[q][e], y[q][e], H, W, tx, ty);
+                c[e] = pack_target(tx, ty, t0x, t0y, bw);
+            }
+            const int64_t p = int64_t(j) * W + i0;
+            if constexpr (kVec) {
+                *reinterpret_cast<uint2 *>(cb + p) =
+                    make_uint2(unsigned(c[0]) | (unsigned(c[1]) << 16), unsigned(c[2]) | (unsigned(c[3]) << 16));
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (i0 + e < W) cb[p + e] = c[e];
+            }
+        }
+    }
     if (lane == 0)
         ws.segrec[sgg] = (smn & 0xFFFFu) == 0xFFFFu
                              ? empty_box()
@@ -788,7 +851,7 @@ struct BinMinW<EgoCoords<D>> {
     static constexpr int value = 1;
 };
 
-template <typename Coords, bool kVec, int kSPW = 1>
+template <typename Coords, bool kVec, int kSPW = 1, bool kPack = false>
 __global__ __launch_bounds__(kWarpThreads, BinMinW<Coords>::value) void bin_kernel(Coords co, const float *__restrict__ depth, ChunkArgs a,
                                                               int H, int W, int64_t HW, TileGeom g) {
     using V = typename Coords::V;
@@ -813,7 +876,7 @@ __global__ __launch_bounds__(kWarpThreads, BinMinW<Coords>::value) void bin_kern
     }
 #pragma unroll
     for (int s = 0; s < kSPW; ++s)
-        if (sg0 + s < nsg) bin_segment(co, depth, a, H, W, HW, g, sg0 + s, x[s], y[s]);  // wave-uniform
+        if (sg0 + s < nsg) bin_segment<Coords, kPack, kVec>(co, depth, a, H, W, HW, g, sg0 + s, x[s], y[s]);  // wave-uniform
 }
 
 // ---- SPLAT.  Workgroup id -> XCD-aware tile: dispatch is round-robin over the
@@ -966,7 +1029,7 @@ __device__ __forceinline__ unsigned dequeue_tile(unsigned *queue, unsigned home,
 // One target tile (linear index `lin` of the chunk's band-major tile order).
 // Every barrier is LDS-only: global loads are consumed by the thread that
 // issued them, and the published stores are never waited for.
-template <typename Coords, bool kVec, bool kFuse, bool kStamp, typename Cfg, typename E = float>
+template <typename Coords, bool kVec, bool kFuse, bool kStamp, typename Cfg, typename E = float, bool kPack = false>
 __device__ __forceinline__ void splat_tile(TileLds &L, unsigned lin, int bl, int tile, const Coords &co,
                                            const float *__restrict__ depth, const SplatIO &io, const ChunkArgs &a,
                                            int H, int W, int64_t HW, const TileGeom &g, unsigned long long *stamps) {
@@ -1001,6 +1064,7 @@ __device__ __forceinline__ void splat_tile(TileLds &L, unsigned lin, int bl, int
     const bool all_blocks = nsel > kSegCap;
     const int ncand = all_blocks ? g.nsb : nsel * SEGB;
     const int lane = lane_id(), wave = threadIdx.x >> 6;
+    [[maybe_unused]] unsigned nblk_tot = 0;  // kStamp: candidate blocks splatted
 
     for (int c0 = 0; c0 < ncand; c0 += kListCap) {
         // ---- 2. candidate blocks whose box holds this tile -> L.blk
@@ -1017,9 +1081,14 @@ __device__ __forceinline__ void splat_tile(TileLds &L, unsigned lin, int bl, int
                     sb = sbx < g.nsbx ? sby * g.nsbx + sbx : -1;
                 }
             }
-            if (sb >= 0 && box_has(blkrec[sb], txi, tyi)) {
-                const unsigned idx = atomicAdd(&L.nblk, 1u);
-                L.blk[idx] = unsigned(sb);
+            if (sb >= 0) {
+                const ushort4 r = blkrec[sb];
+                if (box_has(r, txi, tyi)) {
+                    const unsigned idx = atomicAdd(&L.nblk, 1u);
+                    // kPack: this tile's index in the block's box rides in the top nibble
+                    const unsigned kt = kPack ? unsigned((tyi - int(r.z)) * (int(r.y) - int(r.x) + 1) + (txi - int(r.x))) : 0u;
+                    L.blk[idx] = unsigned(sb) | (kt << 28);
+                }
             }
         }
         lds_barrier();
@@ -1029,7 +1098,63 @@ __device__ __forceinline__ void splat_tile(TileLds &L, unsigned lin, int bl, int
         using V = typename Coords::V;
         constexpr int kU = sizeof(V) == 4 ? Cfg::kUF : 1;  // 64-VGPR budget
         const int nb = int(L.nblk);
+        if constexpr (kStamp) nblk_tot += unsigned(nb);
         const int sub = lane >> 4, rr = (lane >> 2) & 3, c4 = (lane & 3) * 4;
+        if constexpr (kPack) {
+            // packed targets (BIN): 8 bytes of codes + 16 of depth per lane and
+            // slot, no target arithmetic
+            constexpr int kUP = Cfg::kUF;
+            const unsigned short *cb = ws.code + int64_t(bl) * HW;
+            for (int e0 = wave * 4; e0 < nb; e0 += Cfg::kWaves * 4 * kUP) {
+                unsigned cw[kUP][2];
+                float d[kUP][4];
+                int ii[kUP], jj[kUP];
+                unsigned kt[kUP];
+#pragma unroll
+                for (int u = 0; u < kUP; ++u) {
+                    const int e = e0 + sub + u * Cfg::kWaves * 4;
+                    ii[u] = W;
+                    jj[u] = 0;
+                    kt[u] = 0;
+                    if (e < nb) {
+                        const unsigned be = L.blk[e];
+                        const int sb = int(be & 0x0FFFFFFFu);
+                        kt[u] = be >> 28;
+                        const int sby = sb / g.nsbx, sbx = sb - sby * g.nsbx;
+                        const int i = sbx * SBW + c4, j = sby * SBH + rr;
+                        if (i < W && j < H) {
+                            ii[u] = i;
+                            jj[u] = j;
+                            const int64_t p = int64_t(j) * W + i;
+                            if constexpr (kVec) {
+                                const uint2 v = *reinterpret_cast<const uint2 *>(cb + p);
+                                cw[u][0] = v.x;
+                                cw[u][1] = v.y;
+                            } else {
+                                unsigned short c[4];
+#pragma unroll
+                                for (int q = 0; q < 4; ++q) c[q] = i + q < W ? cb[p + q] : CODE_NONE;
+                                cw[u][0] = unsigned(c[0]) | (unsigned(c[1]) << 16);
+                                cw[u][1] = unsigned(c[2]) | (unsigned(c[3]) << 16);
+                            }
+                            co.template load4k<kVec>(b, p, d[u], W - i, depth);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < kUP; ++u) {
+                    if (ii[u] >= W) continue;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int i = ii[u] + q;
+                        if (i >= W) break;
+                        const unsigned c = (cw[u][q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
+                        if ((c >> 12) == kt[u])
+                            atomicMin(&L.zk[c & 0xFFFu], make_key(d[u][q], unsigned(jj[u] * W + i)));
+                    }
+                }
+            }
+        } else
         for (int e0 = wave * 4; e0 < nb; e0 += Cfg::kWaves * 4 * kU) {
             V cx[kU][4], cy[kU][4];
             float d[kU][4];
@@ -1040,7 +1165,7 @@ __device__ __forceinline__ void splat_tile(TileLds &L, unsigned lin, int bl, int
                 ii[u] = W;
                 jj[u] = 0;
                 if (e < nb) {
-                    const int sb = int(L.blk[e]);
+                    const int sb = int(L.blk[e] & 0x0FFFFFFFu);
                     const int sby = sb / g.nsbx, sbx = sb - sby * g.nsbx;
                     const int i = sbx * SBW + c4, j = sby * SBH + rr;
                     if (i < W && j < H) {
@@ -1230,7 +1355,7 @@ __device__ __forceinline__ void splat_tile(TileLds &L, unsigned lin, int bl, int
     }
     if constexpr (kStamp) {
         lds_barrier();
-        if (threadIdx.x == 0) { ph[1] = wall_clock64(); ph[2] = 0; ph[3] = lin; }
+        if (threadIdx.x == 0) { ph[1] = wall_clock64(); ph[2] = nblk_tot; ph[3] = lin; }
     }
 }
 
@@ -1266,7 +1391,7 @@ using FusedCfgFor = typename std::conditional<Coords::kGen == 0, FusedCfg, Fused
 // where the hardware's dispatch of fresh workgroups balances the last tiles
 // better than the persistent kernel's queues (see run_f32).
 template <typename Coords, bool kVec, bool kFuse = false, bool kStamp = false, typename Cfg = SplitCfg,
-          typename E = float>
+          typename E = float, bool kPack = false>
 __global__ __launch_bounds__(Cfg::kThr, Cfg::kMinW) void splat_kernel(Coords co, const float *__restrict__ depth,
                                                                 SplatIO io, ChunkArgs a, int H, int W, int64_t HW,
                                                                 TileGeom g, unsigned long long *stamps = nullptr) {
@@ -1277,7 +1402,7 @@ __global__ __launch_bounds__(Cfg::kThr, Cfg::kMinW) void splat_kernel(Coords co,
     if (lin >= total) return;
     int bl, tile;
     tile_of<Cfg>(lin, a, g, bl, tile);
-    splat_tile<Coords, kVec, kFuse, kStamp, Cfg, E>(L, lin, bl, tile, co, depth, io, a, H, W, HW, g, stamps);
+    splat_tile<Coords, kVec, kFuse, kStamp, Cfg, E, kPack>(L, lin, bl, tile, co, depth, io, a, H, W, HW, g, stamps);
 }
 
 // Persistent SPLAT: one workgroup per resident slot, looping over tiles.  The
@@ -1289,7 +1414,7 @@ __global__ __launch_bounds__(Cfg::kThr, Cfg::kMinW) void splat_kernel(Coords co,
 // Placement and order affect speed only: every tile is processed exactly
 // once, and no workgroup ever waits for another.
 template <typename Coords, bool kVec, bool kFuse = true, bool kStamp = false, typename Cfg = FusedCfg,
-          typename E = float>
+          typename E = float, bool kPack = false>
 __global__ __launch_bounds__(Cfg::kThr, Cfg::kMinW) void splat_persist_kernel(Coords co, const float *__restrict__ depth,
                                                                         SplatIO io, ChunkArgs a, int H, int W,
                                                                         int64_t HW, TileGeom g,
@@ -1307,7 +1432,7 @@ __global__ __launch_bounds__(Cfg::kThr, Cfg::kMinW) void splat_persist_kernel(Co
         if (lin == ~0u) return;
         int bl, tile;
         tile_of<Cfg>(lin, a, g, bl, tile);
-        splat_tile<Coords, kVec, kFuse, kStamp, Cfg, E>(L, lin, bl, tile, co, depth, io, a, H, W, HW, g, stamps);
+        splat_tile<Coords, kVec, kFuse, kStamp, Cfg, E, kPack>(L, lin, bl, tile, co, depth, io, a, H, W, HW, g, stamps);
         // splat_tile ends with LDS reads of the z-buffer; the next iteration's
         // barrier orders them before the next tile's initialisation
     }
@@ -1555,16 +1680,29 @@ unsigned resident_slots(K kernel, int threads) {
     return unsigned(cus) * unsigned(per);
 }
 
-template <typename Coords, bool kVec, typename Cfg = FusedCfgFor<Coords>, typename E = float>
+template <typename Coords, bool kVec, typename Cfg = FusedCfgFor<Coords>, typename E = float, bool kPack = false>
 unsigned persist_slots() {
-    static const unsigned slots = resident_slots(splat_persist_kernel<Coords, kVec, true, false, Cfg, E>, Cfg::kThr);
+    static const unsigned slots =
+        resident_slots(splat_persist_kernel<Coords, kVec, true, false, Cfg, E, kPack>, Cfg::kThr);
     return slots;
 }
 
-template <typename Coords, bool kVec, typename Cfg = FusedCfgFor<Coords>, typename E = float>
+template <typename Coords, bool kVec, typename Cfg = FusedCfgFor<Coords>, typename E = float, bool kPack = false>
 unsigned persist_grid(unsigned tiles) {
-    const unsigned slots = persist_slots<Coords, kVec, Cfg, E>();
+    const unsigned slots = persist_slots<Coords, kVec, Cfg, E, kPack>();
     return tiles < slots ? tiles : slots;
+}
+
+// Packed targets in the fused TILE engine (coordinate sources with exact BIN
+// targets): on by default; OFD_FW_PACK=0 or ofd_fw_set_pack(0) turns them off
+// (A/B and cross-check; results never depend on it).
+int g_pack = -1;
+bool pack_enabled() {
+    if (g_pack < 0) {
+        const char *e = getenv("OFD_FW_PACK");
+        g_pack = e ? (atoi(e) != 0) : 1;
+    }
+    return g_pack != 0;
 }
 
 // Calls with fewer than persist_min() tiles per resident SPLAT slot launch
@@ -1646,38 +1784,49 @@ int run_f32(Coords co, const E *obj, const float *depth, E *out, float *valid, f
             const ChunkArgs a{slab, b0, int(nb)};
             const SplatIO io{valid, coll, obj, out, int(C), int(C) - Coords::kGen, gen_at};
             const dim3 bgrid(grid_for(nb * g.nseg, kWaves * kBinSPW));
+            const dim3 sgrid((unsigned(nb * g.ntiles) + 7u) / 8u * 8u);
+            if (mode == Mode::Tile) {
+                // fused: BIN, then a persistent SPLAT gathers the output planes
+                // itself (dominant kernel); one SPLAT workgroup per tile on
+                // short calls
+                const unsigned tiles = unsigned(nb * g.ntiles);
+                using Cfg = FusedCfgFor<Coords>;
+                auto fused = [&](auto vec_c, auto pack_c) {
+                    constexpr bool kV = decltype(vec_c)::value, kP = decltype(pack_c)::value;
+                    hipLaunchKernelGGL((bin_kernel<Coords, kV, kBinSPW, kP>), bgrid, dim3(kWarpThreads), 0, st, co,
+                                       depth, a, int(H), int(W), HW, g);
+                    if (c == 0 && g_prof_start) (void)hipEventRecord(g_prof_start, st);
+                    if (tiles < persist_min() * persist_slots<Coords, kV, Cfg, E, kP>())
+                        hipLaunchKernelGGL((splat_kernel<Coords, kV, true, false, Cfg, E, kP>), sgrid, dim3(Cfg::kThr),
+                                           0, st, co, depth, io, a, int(H), int(W), HW, g, nullptr);
+                    else
+                        hipLaunchKernelGGL((splat_persist_kernel<Coords, kV, true, false, Cfg, E, kP>),
+                                           dim3(persist_grid<Coords, kV, Cfg, E, kP>(tiles)), dim3(Cfg::kThr), 0, st,
+                                           co, depth, io, a, int(H), int(W), HW, g, nullptr);
+                };
+                using T_ = std::true_type;
+                using F_ = std::false_type;
+                bool packed = false;
+                if constexpr (Coords::kPackable) {
+                    if (pack_enabled()) {
+                        packed = true;
+                        if (vec) fused(T_{}, T_{});
+                        else fused(F_{}, T_{});
+                    }
+                }
+                if (!packed) {
+                    if (vec) fused(T_{}, F_{});
+                    else fused(F_{}, F_{});
+                }
+                if (c == nch - 1 && g_prof_stop) (void)hipEventRecord(g_prof_stop, st);
+                continue;
+            }
             if (vec)
                 hipLaunchKernelGGL((bin_kernel<Coords, true, kBinSPW>), bgrid, dim3(kWarpThreads), 0, st, co, depth, a,
                                    int(H), int(W), HW, g);
             else
                 hipLaunchKernelGGL((bin_kernel<Coords, false, kBinSPW>), bgrid, dim3(kWarpThreads), 0, st, co, depth,
                                    a, int(H), int(W), HW, g);
-            const dim3 sgrid((unsigned(nb * g.ntiles) + 7u) / 8u * 8u);
-            if (mode == Mode::Tile) {
-                // fused: a persistent SPLAT gathers the output planes itself (dominant kernel)
-                const unsigned tiles = unsigned(nb * g.ntiles);
-                if (c == 0 && g_prof_start) (void)hipEventRecord(g_prof_start, st);
-                using Cfg = FusedCfgFor<Coords>;
-                const bool per_tile = vec ? tiles < persist_min() * persist_slots<Coords, true, Cfg, E>()
-                                          : tiles < persist_min() * persist_slots<Coords, false, Cfg, E>();
-                if (per_tile) {
-                    if (vec)
-                        hipLaunchKernelGGL((splat_kernel<Coords, true, true, false, Cfg, E>), sgrid, dim3(Cfg::kThr),
-                                           0, st, co, depth, io, a, int(H), int(W), HW, g, nullptr);
-                    else
-                        hipLaunchKernelGGL((splat_kernel<Coords, false, true, false, Cfg, E>), sgrid, dim3(Cfg::kThr),
-                                           0, st, co, depth, io, a, int(H), int(W), HW, g, nullptr);
-                } else if (vec)
-                    hipLaunchKernelGGL((splat_persist_kernel<Coords, true, true, false, Cfg, E>),
-                                       dim3(persist_grid<Coords, true, Cfg, E>(tiles)), dim3(Cfg::kThr), 0, st, co, depth, io,
-                                       a, int(H), int(W), HW, g, nullptr);
-                else
-                    hipLaunchKernelGGL((splat_persist_kernel<Coords, false, true, false, Cfg, E>),
-                                       dim3(persist_grid<Coords, false, Cfg, E>(tiles)), dim3(Cfg::kThr), 0, st, co, depth, io,
-                                       a, int(H), int(W), HW, g, nullptr);
-                if (c == nch - 1 && g_prof_stop) (void)hipEventRecord(g_prof_stop, st);
-                continue;
-            }
             if constexpr (!kTileOnly) {
             if (vec)
                 hipLaunchKernelGGL((splat_kernel<Coords, true>), sgrid, dim3(kWarpThreads), 0, st, co, depth, io, a,
@@ -1846,6 +1995,12 @@ int ofd_fw_set_disparity_rows(int on) {
 int ofd_fw_set_persist_min(int tiles_per_slot) {
     const int prev = int(persist_min());
     if (tiles_per_slot >= 0) g_persist_min = tiles_per_slot;
+    return prev;
+}
+
+int ofd_fw_set_pack(int on) {
+    const int prev = pack_enabled() ? 1 : 0;
+    if (on == 0 || on == 1) g_pack = on;
     return prev;
 }
 

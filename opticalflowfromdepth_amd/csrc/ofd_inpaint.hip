@@ -1251,9 +1251,9 @@ __global__ __launch_bounds__(256) void ip_hole_tail_kernel(Chunk ch, const uint3
                 const unsigned need = (t / kTailParts) * kTailParts;
                 for (unsigned spins = 0;; ++spins) {
                     unsigned done = 0u;
-                    // polled with an atomic read-modify-write (+0), like every
-                    // other access to the counter
-                    if (lane == 0u) done = atomicAdd(&meta[2], 0u);
+                    // the polling lane's agent-scope acquire load pairs with
+                    // the publishing thread's release add below
+                    if (lane == 0u) done = __hip_atomic_load(&meta[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
                     done = __builtin_amdgcn_readfirstlane(done);
                     if (done >= need) break;
                     if (spins >= kTailSpinBound) {
@@ -1277,9 +1277,13 @@ __global__ __launch_bounds__(256) void ip_hole_tail_kernel(Chunk ch, const uint3
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the previous layers' T and colours
         hole_layer_body(ch, list, hist, cursor, nring, L0 + t / kTailParts, range, thin_cap, patch, t % kTailParts,
                         kTailParts);
+        // every wave completes its own stores (vmcnt is per wave), the barrier
+        // orders them before thread 0, whose agent-scope release add publishes
+        // the part (HIP / HSA memory model: release after the barrier, on the
+        // publishing thread)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         __syncthreads();
-        if (threadIdx.x == 0) atomicAdd(&meta[2], 1u);
+        if (threadIdx.x == 0) __hip_atomic_fetch_add(&meta[2], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 

@@ -1939,25 +1939,48 @@ __global__ __launch_bounds__(256) void sq_unpack_kernel(SqWs w, float *__restric
 
 
 // Helper streams and events of the grouped sequential fill (seq_groups), one
-// set per process (created on first use on the current device).
+// set per device, created on that device on first use.  A call uses the set
+// of its stream's device (hipStreamGetDevice), so its group launches always
+// run on the device that owns the workspace, image and output pointers,
+// whichever device is current.
 struct SeqHelpers {
     std::mutex mu;
+    int device = -1;  // created for this device (-1: not yet)
     bool ok = false;
     hipStream_t stream[3] = {nullptr, nullptr, nullptr};
     hipEvent_t fork = nullptr, join[3] = {nullptr, nullptr, nullptr};
 };
+constexpr int kMaxSeqDevices = 64;
 
-SeqHelpers &seq_helpers() {
-    static SeqHelpers h;
-    static std::once_flag once;
-    std::call_once(once, [] {
-        bool ok = hipEventCreateWithFlags(&h.fork, hipEventDisableTiming) == hipSuccess;
+// The device a call on stream st runs on: the stream's own (the null stream's
+// is the current device); -1 when it cannot be told.
+int stream_device(hipStream_t st) {
+    int dev = -1;
+    if (hipStreamGetDevice(st, &dev) != hipSuccess) {
+        (void)hipGetLastError();
+        if (hipGetDevice(&dev) != hipSuccess) return -1;
+    }
+    return dev;
+}
+
+SeqHelpers *seq_helpers(int dev) {
+    static SeqHelpers h[kMaxSeqDevices];
+    static std::mutex mu;
+    if (dev < 0 || dev >= kMaxSeqDevices) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    SeqHelpers &x = h[dev];
+    if (x.device < 0) {
+        int prev = -1;
+        bool ok = hipGetDevice(&prev) == hipSuccess && (prev == dev || hipSetDevice(dev) == hipSuccess);
+        ok = ok && hipEventCreateWithFlags(&x.fork, hipEventDisableTiming) == hipSuccess;
         for (int k = 0; k < 3 && ok; ++k)
-            ok = hipStreamCreateWithFlags(&h.stream[k], hipStreamNonBlocking) == hipSuccess &&
-                 hipEventCreateWithFlags(&h.join[k], hipEventDisableTiming) == hipSuccess;
-        h.ok = ok;
-    });
-    return h;
+            ok = hipStreamCreateWithFlags(&x.stream[k], hipStreamNonBlocking) == hipSuccess &&
+                 hipEventCreateWithFlags(&x.join[k], hipEventDisableTiming) == hipSuccess;
+        if (prev >= 0 && prev != dev) (void)hipSetDevice(prev);
+        x.ok = ok;
+        x.device = dev;
+    }
+    return &x;
 }
 
 // Groups of the batch (OFD_SEQ_GROUPS, default 1; at most 4): only when
@@ -1999,6 +2022,12 @@ unsigned ofd_sq_fault_read(int reset) {
 }
 
 extern "C" {
+
+int ofd_inpaint_seq_helper_device(void *stream) {
+    const int dev = stream_device(static_cast<hipStream_t>(stream));
+    SeqHelpers *h = seq_helpers(dev);
+    return h && h->ok ? h->device : -1;
+}
 
 int ofd_inpaint_seq_set_groups(int groups) {
     const int prev = seq_groups_setting();
@@ -2088,8 +2117,9 @@ int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float 
         const SqWs w = carve(workspace, G, H, W);
         for (int64_t b0 = 0; b0 < B; b0 += G) run_chunk(w, b0, B - b0 < G ? B - b0 : G, st);
     } else {
-        SeqHelpers &hp = seq_helpers();
-        if (!hp.ok) return OFD_FW_EWORKSPACE;
+        SeqHelpers *hpp = seq_helpers(stream_device(st));
+        if (!hpp || !hpp->ok) return OFD_FW_EWORKSPACE;
+        SeqHelpers &hp = *hpp;
         // one caller at a time enqueues on the shared helper streams: each
         // event's record / wait pair must not interleave with another's
         std::lock_guard<std::mutex> lk(hp.mu);

@@ -19,6 +19,7 @@ LZ77 matches: ~2.3x on these planes against zlib level 6's ~2.9x).
 """
 from __future__ import annotations
 
+import contextlib
 import io
 import os
 import struct
@@ -106,8 +107,46 @@ def member_from_array(key: str, value, level: int = 6) -> _Member:
     return _Member(key + ".npy", zlib.crc32(raw), len(raw), [_raw_deflate(raw, level, final=True)])
 
 
+@contextlib.contextmanager
+def atomic_path(path: str):
+    """A temporary name beside ``path``, renamed onto it (os.replace) only
+    once the body has written it completely: an interrupted run leaves no
+    truncated product file for ``--skip-existing`` to count as done."""
+    tmp = f"{path}.tmp{os.getpid()}.{threading.get_ident()}"
+    try:
+        yield tmp
+        os.replace(tmp, path)
+    except BaseException:
+        try:
+            os.unlink(tmp)
+        except FileNotFoundError:
+            pass
+        raise
+
+
+def zip_complete(path: str) -> bool:
+    """The file ends with a zip end-of-central-directory record (22 bytes, no
+    comment: every writer here and np.savez_compressed end so), i.e. its
+    writer finished it."""
+    try:
+        with open(path, "rb") as f:
+            f.seek(0, os.SEEK_END)
+            if f.tell() < 22:
+                return False
+            f.seek(-22, os.SEEK_END)
+            return f.read(4) == b"PK\x05\x06"
+    except OSError:
+        return False
+
+
 def write_zip(path: str, members: Sequence[_Member]) -> int:
-    """A zip (deflate method) of the members, as zipfile writes one; returns the bytes written."""
+    """A zip (deflate method) of the members, as zipfile writes one; returns
+    the bytes written.  Written under a temporary name and renamed."""
+    with atomic_path(path) as tmp:
+        return _write_zip(tmp, members)
+
+
+def _write_zip(path: str, members: Sequence[_Member]) -> int:
     with open(path, "wb") as f:
         central = []
         for m in members:
@@ -236,23 +275,33 @@ class GpuNpzWriter:
                 while self.pending > 0 and self.pending + total > self.cap:
                     self.cv.wait()
                 self.pending += total
-            host = torch.empty(total, dtype=torch.uint8, pin_memory=True)
-            with torch.cuda.device(dev), torch.cuda.stream(side):
-                side.wait_event(ev_sizes)
+            handed = 0  # bytes whose write job owns their share of `pending`
+            try:
+                host = torch.empty(total, dtype=torch.uint8, pin_memory=True)
+                with torch.cuda.device(dev), torch.cuda.stream(side):
+                    side.wait_event(ev_sizes)
+                    o = 0
+                    for i, n in enumerate(sz):  # the streams, back to back, one D2H each
+                        host[o:o + n].copy_(out[i * bound:i * bound + n], non_blocking=True)
+                        o += n
+                    ev = torch.cuda.Event()
+                    ev.record(side)
+                ev.synchronize()
                 o = 0
-                for i, n in enumerate(sz):  # the streams, back to back, one D2H each
-                    host[o:o + n].copy_(out[i * bound:i * bound + n], non_blocking=True)
+                for i, n in enumerate(sz):
+                    fut = self.pool.submit(write_one, host, i, o, n, cr[i])
+                    handed += n
+                    fut.add_done_callback(lambda f, n=n: done(f, n))
+                    with self._lock:
+                        self.futures.append(fut)
                     o += n
-                ev = torch.cuda.Event()
-                ev.record(side)
-            ev.synchronize()
-            o = 0
-            for i, n in enumerate(sz):
-                fut = self.pool.submit(write_one, host, i, o, n, cr[i])
-                fut.add_done_callback(lambda f, n=n: done(f, n))
-                with self._lock:
-                    self.futures.append(fut)
-                o += n
+            except BaseException:
+                # give back the share no write job will release, so later
+                # fetches and flush() never wait on it
+                with self.cv:
+                    self.pending -= total - handed
+                    self.cv.notify_all()
+                raise
 
         fut = self.fetcher.submit(fetch)
         with self._lock:
@@ -269,15 +318,23 @@ class GpuNpzWriter:
         self.save_batch([path], arrays[k0].unsqueeze(0), k0, extra)
 
     def flush(self) -> None:
-        # a fetch job appends its files' jobs before it completes, so drain
-        # until no job is left
+        """Wait for every pending file, then re-raise the first error.  A
+        fetch job appends its files' jobs before it completes, so drain until
+        no job is left; a failed job never stops the wait for the others."""
+        first = None
         while True:
             with self._lock:
                 futs, self.futures = self.futures, []
             if not futs:
-                return
+                break
             for f in futs:
-                f.result()
+                try:
+                    f.result()
+                except BaseException as e:  # noqa: BLE001 - re-raised below
+                    if first is None:
+                        first = e
+        if first is not None:
+            raise first
 
     def close(self) -> None:
         self.flush()

@@ -32,6 +32,7 @@ from torch import nn
 
 from . import synth
 from .fw import FW
+from .npz_gpu import atomic_path, zip_complete
 from .ops import ego_flow, inpaint, warp_disparity, warp_flow_cat
 from .synth import fix_warped_depth, get_random, normalize_depth
 
@@ -575,11 +576,18 @@ def write_npz(path: str, compresslevel: int = 6, **arrays) -> None:
     by np.load) with a chosen zlib level; level 6 is numpy's own."""
     import zipfile
     from numpy.lib import format as npformat
-    with zipfile.ZipFile(path, mode="w", compression=zipfile.ZIP_DEFLATED, compresslevel=compresslevel,
-                         allowZip64=True) as zf:
+    with atomic_path(path) as tmp, zipfile.ZipFile(tmp, mode="w", compression=zipfile.ZIP_DEFLATED,
+                                                   compresslevel=compresslevel, allowZip64=True) as zf:
         for k, v in arrays.items():
             with zf.open(k + ".npy", mode="w", force_zip64=True) as f:
                 npformat.write_array(f, np.asanyarray(v), allow_pickle=False)
+
+
+def savez_compressed(path: str, **arrays) -> None:
+    """np.savez_compressed (preprocess.py:446, :471-476) into a temporary file
+    renamed onto ``path`` once complete."""
+    with atomic_path(path) as tmp, open(tmp, "wb") as f:
+        np.savez_compressed(f, **arrays)
 
 
 class NpzWriter:
@@ -633,10 +641,17 @@ class NpzWriter:
         self.futures.append(self.pool.submit(job))
 
     def flush(self) -> None:
-        """Wait for every pending file; re-raise the first write error."""
+        """Wait for every pending file, then re-raise the first write error."""
         futs, self.futures = self.futures, []
+        first = None
         for f in futs:
-            f.result()
+            try:
+                f.result()
+            except BaseException as e:  # noqa: BLE001 - re-raised below
+                if first is None:
+                    first = e
+        if first is not None:
+            raise first
 
     def close(self) -> None:
         self.flush()
@@ -657,7 +672,7 @@ def save_group(out_dirs: Sequence[str], group44: torch.Tensor, writer: Optional[
         if writer is not None:
             writer.save(path, img_depth_flow=x)
         else:
-            np.savez_compressed(path, img_depth_flow=x.cpu().numpy())
+            savez_compressed(path, img_depth_flow=x.cpu().numpy())
 
 
 def save_augment(out_dirs: Sequence[str], g: int, a: int, kind: int, d1: torch.Tensor, d2: torch.Tensor,
@@ -676,7 +691,7 @@ def save_augment(out_dirs: Sequence[str], g: int, a: int, kind: int, d1: torch.T
             if writer is not None:
                 writer.save(path, img_depth_flow=x, augment_flow_type=np.array(kind))
             else:
-                np.savez_compressed(path, img_depth_flow=x.cpu().numpy(), augment_flow_type=kind)
+                savez_compressed(path, img_depth_flow=x.cpu().numpy(), augment_flow_type=kind)
 
 
 # ---------------------------------------------------------------- driver (preprocess.py:508-561)
@@ -684,11 +699,14 @@ N_FILES_PER_IMAGE = 1 + 2 * N_GROUPS * len(AUGMENT_SCHEDULE)  # group.npz + 120 
 
 
 def image_complete(d: str, schedule: Sequence[int] = AUGMENT_SCHEDULE, augment: bool = True) -> bool:
-    """Every product file of one image exists (resume: --skip-existing)."""
+    """Every product file of one image exists and was finished (resume:
+    --skip-existing).  The writers rename a file into place only once it is
+    complete; a file that still ends without a zip end record (e.g. left by
+    an older, interrupted writer) makes the image incomplete."""
     names = ["group.npz"]
     if augment:
         names += [f"{g}_{a}_{k}.npz" for g in range(N_GROUPS) for a in range(len(schedule)) for k in (1, 2)]
-    return all(os.path.exists(os.path.join(d, n)) for n in names)
+    return all(zip_complete(os.path.join(d, n)) for n in names)
 
 
 def make_writer(kind: str):

@@ -52,14 +52,50 @@ def test_file_inventory_matches_reference_layout(tmp_path):
     d = tmp_path / "7"
     d.mkdir()
     assert not pp.image_complete(str(d))
-    (d / "group.npz").write_bytes(b"")
+    pp.savez_compressed(str(d / "group.npz"), img_depth_flow=np.zeros((44, 2, 3), np.float32))
     assert pp.image_complete(str(d), augment=False)
     assert not pp.image_complete(str(d))
     for g in range(pp.N_GROUPS):
         for a in range(len(pp.AUGMENT_SCHEDULE)):
             for k in (1, 2):
-                (d / f"{g}_{a}_{k}.npz").write_bytes(b"")
+                pp.write_npz(str(d / f"{g}_{a}_{k}.npz"), 1, img_depth_flow=np.ones((8, 2, 3)),
+                             augment_flow_type=np.array(a))
     assert pp.image_complete(str(d))
+    assert sorted(os.listdir(d)) == sorted(["group.npz"] + [f"{g}_{a}_{k}.npz" for g in range(pp.N_GROUPS)
+                                                            for a in range(len(pp.AUGMENT_SCHEDULE)) for k in (1, 2)])
+    # a truncated file (a writer killed mid-write before the atomic rename existed)
+    # or an empty one makes the image incomplete, so --skip-existing redoes it
+    f = d / "3_5_2.npz"
+    data = f.read_bytes()
+    f.write_bytes(data[:-30])
+    assert not pp.image_complete(str(d))
+    f.write_bytes(b"")
+    assert not pp.image_complete(str(d))
+    f.write_bytes(data)
+    assert pp.image_complete(str(d))
+
+
+def test_writers_never_leave_a_partial_file(tmp_path):
+    from opticalflowfromdepth_amd import npz_gpu
+    path = tmp_path / "x.npz"
+    # a write that fails midway leaves neither the file nor its temporary
+    with pytest.raises(RuntimeError):
+        with npz_gpu.atomic_path(str(path)) as tmp:
+            open(tmp, "wb").write(b"PK partial")
+            raise RuntimeError("killed")
+    assert os.listdir(tmp_path) == []
+
+    class Boom:  # np.lib.format.write_array raises on it after the zip is opened
+        def __array__(self, *a, **k):
+            raise RuntimeError("array failed")
+    with pytest.raises(RuntimeError):
+        pp.write_npz(str(path), 1, img_depth_flow=Boom())
+    assert os.listdir(tmp_path) == []
+    # the zip writer of the GPU writer: a complete file under the final name only
+    m = npz_gpu.member_from_array("a", np.arange(10))
+    n = npz_gpu.write_zip(str(path), [m])
+    assert os.listdir(tmp_path) == ["x.npz"] and os.path.getsize(path) == n and npz_gpu.zip_complete(str(path))
+    assert np.array_equal(np.load(path)["a"], np.arange(10))
 
 
 def test_writer_choice():

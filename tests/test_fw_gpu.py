@@ -353,3 +353,78 @@ def test_tile_engine_overflow_and_wide_boxes(cuda_device):
     depth = rng.integers(1, 5, (B, 1, H, W)).astype(np.float32)
     got = forward_warp_flow(_t(obj, cuda_device), _t(flow, cuda_device), _t(depth, cuda_device))
     _assert_same(got, oracle.fw_flow(obj, flow, depth), "overflow")
+
+
+# ------------------------------------------------------------------ packed targets (BIN -> SPLAT)
+@pytest.fixture
+def unpacked():
+    """The TILE engine with SPLAT re-reading the coordinate planes instead of
+    BIN's 16-bit packed targets (ofd_fw_set_pack(0)): the round-4 path, kept
+    as a cross-check of the default."""
+    from opticalflowfromdepth_amd import _native
+    lib = _native.lib()
+    prev = lib.ofd_fw_set_pack(0)
+    yield
+    lib.ofd_fw_set_pack(prev)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_unpacked_targets_random_vs_oracle(cuda_device, unpacked, seed):
+    from opticalflowfromdepth_amd import forward_warp_flow
+    rng = np.random.default_rng(700 + seed)
+    B, C = int(rng.integers(1, 4)), int(rng.choice([1, 2, 6, 7]))
+    H, W = int(rng.integers(1, 90)), int(rng.integers(1, 120))
+    obj = rng.standard_normal((B, C, H, W)).astype(np.float32)
+    flow = (rng.standard_normal((B, 2, H, W)) * rng.uniform(0.1, 80)).astype(
+        np.float64 if seed % 2 else np.float32)
+    depth = (rng.integers(0, 6, (B, 1, H, W)) * 0.5).astype(np.float32)
+    depth[rng.random(depth.shape) < 0.02] = np.nan
+    got = forward_warp_flow(_t(obj, cuda_device), _t(flow, cuda_device), _t(depth, cuda_device))
+    _assert_same(got, oracle.fw_flow(obj, flow, depth), f"unpacked seed{seed}")
+
+
+def test_packed_and_unpacked_targets_agree(cuda_device):
+    """Every coordinate source that packs (FW on float32 / float64 flows, the
+    op's safe coordinates, warp_flow_cat) gives the same bits with and without
+    packed targets, on the persistent SPLAT (headline-like batch) and the
+    one-workgroup-per-tile SPLAT, on rows with and without 16-byte alignment,
+    with clamped border hot spots and wide (spilled) blocks."""
+    import fw_cuda
+    from opticalflowfromdepth_amd import _native, forward_warp_flow, synth, warp_flow_cat
+    lib = _native.lib()
+    obj, flow, depth = synth.stage_one_batch([12345 + i for i in range(24)], 384, 512, cuda_device)
+    rng = np.random.default_rng(5)
+    wild = flow[:2].clone()
+    wild[0, 0] += 4000.0                                                       # hot spot on column W-1
+    wild[1] += torch.from_numpy((rng.standard_normal((2, 384, 512)) * 120).astype(np.float32)).to(cuda_device)
+    odd = synth.stage_one_batch([999, 1000], 93, 157, cuda_device)             # W % 4 != 0: scalar path
+    sy = flow[:3, 1:2].clone()
+    sx = flow[:3, 0:1].clone()
+    ii = torch.arange(512, device=cuda_device, dtype=torch.float32)
+    jj = torch.arange(384, device=cuda_device, dtype=torch.float32)[:, None]
+    sx = (sx + ii).clamp(0, 511).trunc()
+    sy = (sy + jj).clamp(0, 383).trunc()
+    calls = [
+        lambda: forward_warp_flow(obj, flow, depth),
+        lambda: forward_warp_flow(obj, flow.double(), depth),
+        lambda: forward_warp_flow(obj[:2], wild, depth[:2]),
+        lambda: forward_warp_flow(*odd),
+        lambda: fw_cuda.forward_warping(obj[:3].contiguous(), sy.contiguous(), sx.contiguous(),
+                                        depth[:3].contiguous()),
+        lambda: warp_flow_cat(obj[:, 0:3].contiguous(), flow, depth.double()),
+    ]
+    prev = lib.ofd_fw_set_pack(-1)
+    prev_pm = lib.ofd_fw_set_persist_min(-1)
+    try:
+        for persist_min in (prev_pm, 0, 1000):   # default split, always persistent, always one per tile
+            lib.ofd_fw_set_persist_min(persist_min)
+            for k, call in enumerate(calls):
+                lib.ofd_fw_set_pack(1)
+                a = call()
+                lib.ofd_fw_set_pack(0)
+                b = call()
+                for x, y in zip(a, b):
+                    assert torch.equal(x, y), (persist_min, k)
+    finally:
+        lib.ofd_fw_set_pack(prev)
+        lib.ofd_fw_set_persist_min(prev_pm)

@@ -9,8 +9,8 @@
   layered restatement bit for bit, and the two restatements must stay close on
   smooth images (the bound below is the documented divergence).
 """
+import ctypes
 import os
-
 import time
 
 import numpy as np
@@ -526,3 +526,19 @@ def test_inpaint_sequential_stream_groups_concurrent_callers():
         lib.ofd_inpaint_seq_set_groups(prev)
     for i in range(2):
         assert np.array_equal(got[i], ref[i])
+
+
+@pytest.mark.gpu
+def test_inpaint_sequential_helpers_follow_the_stream_device(cuda_device):
+    """The grouped fill's helper streams are kept per device and chosen by the
+    caller's stream's device: a call on a stream of device d
+    forks onto helpers created on d, whichever device is current."""
+    from opticalflowfromdepth_amd import _native
+    lib = _native.lib()
+    for d in range(torch.cuda.device_count()):
+        with torch.cuda.device(d):
+            s = torch.cuda.Stream()
+        with torch.cuda.device(0):  # current device 0, stream on d
+            assert lib.ofd_inpaint_seq_helper_device(ctypes.c_void_p(s.cuda_stream)) == d
+        with torch.cuda.device(d):
+            assert lib.ofd_inpaint_seq_helper_device(None) == d  # the null stream: the current device

@@ -98,6 +98,11 @@ def test_schedule_setters_are_host_state():
     assert lib.ofd_fw_set_persist_min(7) == cur
     assert lib.ofd_fw_set_persist_min(-1) == 7
     lib.ofd_fw_set_persist_min(cur)
+    pk = lib.ofd_fw_set_pack(-1)
+    assert pk in (0, 1)
+    assert lib.ofd_fw_set_pack(1 - pk) == pk
+    assert lib.ofd_fw_set_pack(7) == 1 - pk  # only queries
+    lib.ofd_fw_set_pack(pk)
     g = lib.ofd_inpaint_seq_set_groups(-1)
     assert 1 <= g <= 4
     assert lib.ofd_inpaint_seq_set_groups(9) == g

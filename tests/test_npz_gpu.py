@@ -158,6 +158,42 @@ def test_gpu_npz_writer_reports_a_failed_write(cuda_device, tmp_path):
 
 
 @pytest.mark.gpu
+def test_gpu_npz_writer_recovers_from_a_failed_fetch(cuda_device, tmp_path):
+    """A fetch job that fails after taking its share of the pending-bytes cap
+    (here: handing the second file to the pool raises) gives back the share
+    no write job will release: flush raises the error after
+    waiting for every job, and a later batch under the same small cap is
+    written instead of waiting forever."""
+    from opticalflowfromdepth_amd.npz_gpu import GpuNpzWriter
+    x = torch.randn(3, 8, 32, 40, device=cuda_device)
+    w = GpuNpzWriter(workers=2, max_pending_bytes=1)  # any leaked share would block the next fetch
+    real_submit, calls = w.pool.submit, []
+
+    def flaky_submit(fn, *a, **k):
+        calls.append(1)
+        if len(calls) == 2:
+            raise RuntimeError("submit failed")
+        return real_submit(fn, *a, **k)
+    w.pool.submit = flaky_submit
+    w.save_batch([str(tmp_path / f"a{i}.npz") for i in range(3)], x)
+    with pytest.raises(RuntimeError, match="submit failed"):
+        w.flush()
+    import time
+    t0 = time.time()
+    while w.pending and time.time() - t0 < 10:  # done-callbacks run just after result() returns
+        time.sleep(0.01)
+    assert w.pending == 0
+    w.pool.submit = real_submit
+    w.save_batch([str(tmp_path / f"b{i}.npz") for i in range(3)], x)
+    w.close()
+    xs = x.cpu().numpy()
+    for i in range(3):
+        assert np.array_equal(np.load(str(tmp_path / f"b{i}.npz"))["img_depth_flow"], xs[i])
+    assert np.array_equal(np.load(str(tmp_path / "a0.npz"))["img_depth_flow"], xs[0])
+    assert not any(".tmp" in f for f in os.listdir(tmp_path))
+
+
+@pytest.mark.gpu
 def test_pipeline_files_with_gpu_writer_equal_zlib_writer(cuda_device, tmp_path):
     """run_batch writing its 121 files per image through the GPU writer: every
     array np.load-equal to the same run through the zlib NpzWriter."""

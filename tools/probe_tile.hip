@@ -13,6 +13,7 @@
 //         8 = persistent fused SPLAT (stamped)    9 = persistent fused SPLAT
 //        10..14 = fused SPLAT launch-shape variants (see the cases)
 //         2 = RESOLVE (product shape)
+//        15 = BIN writing packed targets, 16 / 17 = packed persistent fused SPLAT (stamped / not)
 using C256 = SplatCfg<256, 8, 4>;
 using C512u3 = SplatCfg<512, 8, 4, 3>;
 using C256u3 = SplatCfg<256, 8, 4, 3>;
@@ -61,6 +62,14 @@ extern "C" int probe_launch(int which, const float *obj, const float *flow, cons
                            dim3(P::kThr), 0, st, co, depth, io, a, int(H), int(W), HW, g, nullptr);
         break;
     }
+    case 15: hipLaunchKernelGGL((bin_kernel<Co, true, 1, true>), dim3(grid_for(nsg, kWaves)), blk, 0, st, co, depth, a,
+                                int(H), int(W), HW, g); break;  // BIN writing packed targets
+    case 16: hipLaunchKernelGGL((splat_persist_kernel<Co, true, true, true, FusedCfg, float, true>),
+                                dim3(persist_grid<Co, true, FusedCfg, float, true>(sgrid.x)), dim3(FusedCfg::kThr), 0, st,
+                                co, depth, io, a, int(H), int(W), HW, g, stamps); break;  // packed, stamped
+    case 17: hipLaunchKernelGGL((splat_persist_kernel<Co, true, true, false, FusedCfg, float, true>),
+                                dim3(persist_grid<Co, true, FusedCfg, float, true>(sgrid.x)), dim3(FusedCfg::kThr), 0, st,
+                                co, depth, io, a, int(H), int(W), HW, g, nullptr); break;  // packed
     case 2:
         hipLaunchKernelGGL((resolve2d_kernel<8, kResolveRows, kResolveWX, true, true>),
                            dim3(unsigned((W + 64 * kResolveWX - 1) / (64 * kResolveWX)),
