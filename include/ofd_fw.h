@@ -29,6 +29,9 @@
  *       Convert.depth_to_random_flow (preprocess.py:265-298) with
  *       geometry.BackprojectDepth / Project3D (geometry.py:17-67): the
  *       ego-motion flow plane from depth, inv_K and P = (K @ T)[:3].
+ *   ofd_fw_rotation_flow_f32
+ *       SpecialFlow._rotate's special / back special flows
+ *       (preprocess.py:31-41, :63-77), one kernel for a batch.
  *   ofd_fw_warp_ego_f32 / _f64depth
  *       preprocess.py:371-373 / :385-387 (ego-motion flow, the obj
  *       concatenation and the FW call) fused into one warp.
@@ -218,6 +221,16 @@ int ofd_fw_ego_flow_f32(const float *depth, const float *P, const float *inv_K, 
                         int64_t W, void *stream);
 int ofd_fw_ego_flow_f64depth(const double *depth, const float *P, const float *inv_K, float *flow, int64_t B,
                              int64_t H, int64_t W, void *stream);
+
+/* SpecialFlow._rotate (preprocess.py:31-41, :63-77): the rotation special
+ * flow and back special flow [B,2,H,W] float32, p1 = (p0 - c0) @ R + c0 minus
+ * p0, for R = rotate / reverse_rotate.  params [B][10] float32 (device):
+ * c0x, c0y, then R and reverse R row-major (R = [[cos t, -sin t], [sin t,
+ * cos t]] as the reference builds it, t and -t).  The 2-term product rounds
+ * as a GEMM accumulates it (k = 0 product, then a fused multiply-add of the
+ * k = 1 term): bit-identical to the reference's matmul. */
+int ofd_fw_rotation_flow_f32(const float *params, float *flow, float *back_flow, int64_t B, int64_t H, int64_t W,
+                             void *stream);
 
 /* Fused depth -> ego-motion flow -> FW (preprocess.py:371-373, :385-387):
  *     flow    = the ofd_fw_ego_flow_* plane

@@ -48,6 +48,7 @@ SIGNATURES = {
     "ofd_fw_warp_disparity_f64depth": ([_P, _I64, _P, _P, _P, _P, _P] + [_I64] * 3 + [_P, _SZ, _P], ctypes.c_int),
     "ofd_fw_ego_flow_f32": ([_P] * 4 + [_I64] * 3 + [_P], ctypes.c_int),
     "ofd_fw_ego_flow_f64depth": ([_P] * 4 + [_I64] * 3 + [_P], ctypes.c_int),
+    "ofd_fw_rotation_flow_f32": ([_P] * 3 + [_I64] * 3 + [_P], ctypes.c_int),
     "ofd_fw_warp_ego_f32": ([_P, _I64] + [_P] * 6 + [_I64] * 3 + [_P, _SZ, _P], ctypes.c_int),
     "ofd_fw_warp_ego_f64depth": ([_P, _I64] + [_P] * 6 + [_I64] * 3 + [_P, _SZ, _P], ctypes.c_int),
     "ofd_fw_warp_flow_cat": ([_P, _I64, _P, ctypes.c_int, _P, ctypes.c_int] + [_P] * 3 + [_I64] * 3 + [_P, _SZ, _P],

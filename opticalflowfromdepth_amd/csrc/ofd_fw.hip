@@ -2141,6 +2141,50 @@ int ego_flow(const D *depth, const float *P, const float *inv_K, float *flow, in
     return e == hipSuccess ? OFD_FW_OK : int(e);
 }
 
+// SpecialFlow._rotate's flows (preprocess.py:31-41, :63-77): p1 = (p0 - c0)
+// @ R + c0, flow = p1 - p0, for R = rotate and reverse_rotate.  The 2-term
+// product is evaluated the way a GEMM accumulates it -- the k = 0 product
+// rounded, then a fused multiply-add of the k = 1 term -- which is the rounding
+// of the reference's matmul (checked bit for bit against its CPU run,
+// tests/golden/ppa_fill_large.npz); the library is built with contraction off,
+// so every other operation rounds on its own.  params [B][10] float32:
+// c0x, c0y, R (r00, r01, r10, r11), reverse R (q00, q01, q10, q11).
+__global__ __launch_bounds__(kBlock) void rotation_flow_kernel(const float *__restrict__ params, float *__restrict__ flow,
+                                                              float *__restrict__ back, int H, int W, int64_t n) {
+    const int64_t q = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+    if (q >= n) return;
+    const int64_t HW = int64_t(H) * W;
+    const int64_t b = q / HW;
+    const int p = int(q - b * HW);
+    const int j = p / W, i = p - j * W;
+    const float *pr = params + b * 10;
+    const float x = float(i), y = float(j);
+    const float dx = x - pr[0], dy = y - pr[1];
+    float *fo = flow + b * 2 * HW + p, *bo = back + b * 2 * HW + p;
+    {
+        const float px = fmaf(dy, pr[4], dx * pr[2]), py = fmaf(dy, pr[5], dx * pr[3]);
+        fo[0] = (px + pr[0]) - x;
+        fo[HW] = (py + pr[1]) - y;
+    }
+    {
+        const float px = fmaf(dy, pr[8], dx * pr[6]), py = fmaf(dy, pr[9], dx * pr[7]);
+        bo[0] = (px + pr[0]) - x;
+        bo[HW] = (py + pr[1]) - y;
+    }
+}
+
+int rotation_flow(const float *params, float *flow, float *back, int64_t B, int64_t H, int64_t W, void *stream) {
+    if (int rc = check_dims(B, 2, H, W)) return rc;
+    if (B * H * W == 0) return OFD_FW_OK;
+    if (!params || !flow || !back) return OFD_FW_EINVAL;
+    if (!aligned(params, 4) || !aligned(flow, 4) || !aligned(back, 4)) return OFD_FW_EALIGN;
+    const int64_t n = B * H * W;
+    hipLaunchKernelGGL(rotation_flow_kernel, dim3(grid_for(n)), dim3(kBlock), 0, static_cast<hipStream_t>(stream),
+                       params, flow, back, int(H), int(W), n);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? OFD_FW_OK : int(e);
+}
+
 template <typename D>
 int warp_ego(const float *obj, int64_t Cobj, const D *depth, const float *P, const float *inv_K, float *output,
              float *valid, float *collision, int64_t B, int64_t H, int64_t W, void *workspace, size_t workspace_bytes,
@@ -2189,6 +2233,11 @@ int ofd_fw_ego_flow_f32(const float *depth, const float *P, const float *inv_K, 
 int ofd_fw_ego_flow_f64depth(const double *depth, const float *P, const float *inv_K, float *flow, int64_t B,
                              int64_t H, int64_t W, void *stream) {
     return ego_flow(depth, P, inv_K, flow, B, H, W, stream);
+}
+
+int ofd_fw_rotation_flow_f32(const float *params, float *flow, float *back_flow, int64_t B, int64_t H, int64_t W,
+                             void *stream) {
+    return rotation_flow(params, flow, back_flow, B, H, W, stream);
 }
 
 int ofd_fw_warp_ego_f32(const float *obj, int64_t Cobj, const float *depth, const float *P, const float *inv_K,

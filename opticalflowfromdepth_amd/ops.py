@@ -387,6 +387,28 @@ def ego_flow(depth: torch.Tensor, P: torch.Tensor, inv_K: torch.Tensor) -> torch
     return flow
 
 
+def rotation_flow(params: torch.Tensor, h: int, w: int, device) -> Tuple[torch.Tensor, torch.Tensor]:
+    """SpecialFlow._rotate's (special_flow, back_special_flow) [B,2,h,w] float32
+    (preprocess.py:31-41, :63-77) on ``device``, from params [B,10] float32:
+    c0x, c0y, rotate and reverse_rotate row-major.  Bit-identical to the
+    reference's matmul (include/ofd_fw.h ofd_fw_rotation_flow_f32)."""
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        raise RuntimeError("rotation_flow needs a HIP device")
+    params = params.to(device=dev, dtype=_F32).contiguous()
+    if params.dim() != 2 or params.shape[1] != 10:
+        raise RuntimeError(f"params must be [B,10], got {tuple(params.shape)}")
+    B = params.shape[0]
+    with torch.cuda.device(dev):
+        stream = torch.cuda.current_stream(dev)
+        flow = torch.empty(B, 2, h, w, dtype=_F32, device=dev)
+        back = torch.empty_like(flow)
+        rc = _native.lib().ofd_fw_rotation_flow_f32(params.data_ptr(), flow.data_ptr(), back.data_ptr(), B, h, w,
+                                                    stream.cuda_stream)
+        _native.check(rc, "rotation_flow")
+    return flow, back
+
+
 def warp_ego(obj: torch.Tensor, depth: torch.Tensor, P: torch.Tensor, inv_K: torch.Tensor,
              out: Tuple[torch.Tensor, torch.Tensor, torch.Tensor] = None
              ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:

@@ -33,7 +33,7 @@ from torch import nn
 from . import synth
 from .fw import FW
 from .npz_gpu import atomic_path, zip_complete
-from .ops import ego_flow, inpaint, warp_disparity, warp_flow_cat
+from .ops import ego_flow, inpaint, rotation_flow, warp_disparity, warp_flow_cat
 from .synth import fix_warped_depth, get_random, normalize_depth
 
 AUGMENT_SCHEDULE = (0, 5, 6, 7, 1, 5, 6, 7, 2, 5, 6, 7)  # preprocess.py:454
@@ -168,8 +168,9 @@ def special_flow_from_params(h, w, kind, params, device) -> Tuple[torch.Tensor, 
     kind 5 = flip (vertical: a fresh SpecialFlow toggles horizontal_flip to
     False, preprocess.py:49-54), 6 = rotate (params [B,3]: cx, cy, theta),
     7 = shear (vertical for a fresh instance, :83-91; params [B]: shear).
-    The 2x2 products of :74-75 / :94-95 are evaluated as separate multiplies
-    and adds (no fused multiply-add)."""
+    The rotation's 2x2 product (:74-75) rounds as the reference's matmul
+    does (ops.rotation_flow on the device); the shear's (:94-95) has a zero
+    term and is a multiply and an add."""
     x, y = _p0(h, w, device)
     if kind >= 7:
         s = params.to(device=device, dtype=torch.float32).view(-1, 1, 1)
@@ -178,16 +179,24 @@ def special_flow_from_params(h, w, kind, params, device) -> Tuple[torch.Tensor, 
         zero = torch.zeros_like(fy)
         return torch.stack((zero, fy), 1), torch.stack((zero, by), 1)
     if kind >= 6:
-        p = params.to(device=device, dtype=torch.float32)
-        cx, cy, th = p[:, 0].view(-1, 1, 1), p[:, 1].view(-1, 1, 1), p[:, 2]
+        # rotate / reverse_rotate built on the host from the drawn theta
+        # exactly as :66-71 build them (torch.cos / sin of the float32 angle
+        # and of its negation), then (p0 - c0) @ R + c0 - p0 per pixel
+        p = params.detach().to(device="cpu", dtype=torch.float32)
+        th = p[:, 2]
+        mats = []
+        for t in (th, -th):
+            c, sn = torch.cos(t), torch.sin(t)
+            mats.append(torch.stack((c, -sn, sn, c), 1))
+        rp = torch.cat((p[:, 0:2], mats[0], mats[1]), 1)                  # [B,10]
+        if torch.device(device).type == "cuda":
+            return rotation_flow(rp, h, w, device)
+        # host tensors: the reference's own matmul, image by image in its shapes
+        p0 = torch.stack((x, y), -1)                                      # [h,w,2]
         out = []
-        for sgn in (1.0, -1.0):
-            t = th * sgn
-            c, sn = torch.cos(t).view(-1, 1, 1), torch.sin(t).view(-1, 1, 1)
-            dx, dy = x - cx, y - cy
-            px = (dx * c + dy * sn) + cx      # [dx, dy] @ [[c, -s], [s, c]] + c0
-            py = (dx * (-sn) + dy * c) + cy
-            out.append(torch.stack((px - x, py - y), 1))
+        for k in (2, 6):
+            fl = [((p0 - rp[b, 0:2]) @ rp[b, k:k + 4].view(2, 2) + rp[b, 0:2]) - p0 for b in range(rp.shape[0])]
+            out.append(torch.stack(fl).permute(0, 3, 1, 2).contiguous())
         return out[0], out[1]
     B = params.shape[0] if params is not None else 1
     fy = (float(h - 1) - y) - y

@@ -208,10 +208,18 @@ def disparity_flow(depth: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
 def projection(h: int, w: int, T: torch.Tensor, device) -> Tuple[torch.Tensor, torch.Tensor]:
     """Project3D's P = (K @ T)[:, :3] (geometry.py:57) on ``device`` [B,3,4], and
     inv_K[:3,:3] (geometry.py:38) as a CPU [3,3] float32 tensor -- the camera
-    inputs of ops.ego_flow / ops.warp_ego."""
+    inputs of ops.ego_flow / ops.warp_ego.
+
+    P is multiplied on the host, one image at a time in the reference's own
+    shapes ([1,4,4] @ [1,4,4]), and then copied to ``device``: with that P the
+    device flow is bit for bit the reference's CPU run (the 4x4 product on
+    the GPU rounds some entries differently, which moved the flow by up to
+    8 ulp; tests/test_ego.py, tests/golden/ppa_fill_large.npz)."""
     K, inv_K = intrinsics(h, w)
-    P = torch.matmul(K.to(device).unsqueeze(0), T.to(device))[:, :3, :].contiguous()
-    return P, inv_K[:3, :3].contiguous()
+    Tc = T.detach().to(device="cpu", dtype=torch.float32)
+    Kc = K.to("cpu").unsqueeze(0)
+    P = torch.cat([torch.matmul(Kc, Tc[b:b + 1]) for b in range(Tc.shape[0])])[:, :3, :]
+    return P.contiguous().to(device), inv_K[:3, :3].contiguous()
 
 
 def ego_motion_flow(depth: torch.Tensor, T: torch.Tensor) -> torch.Tensor:

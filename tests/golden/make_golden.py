@@ -497,7 +497,25 @@ def _tol_channels(key, kind):
     return (4, 5, 6, 7) if key.endswith("_1") else (0, 1, 2, 3)
 
 
-def make_ppa_fill_cases(utils_mod, ref_fw, Convert, h=32, w=40, seeds=(5150, 5151), sample=(5, 7), tol_full=True):
+def _rotation_base(rot, c0, h, w):
+    """numpy evaluation of SpecialFlow._rotate's flow, (p0 - c0) @ rot + c0 -
+    p0 (preprocess.py:63-77), in float32 with the 2-term product rounded as a
+    GEMM accumulates it: the k = 0 product, then a fused multiply-add of the
+    k = 1 term (emulated in float64: the product is exact there, the sum
+    rounds once before the float32 rounding).  The base that
+    ppa_fill_large.npz's rotation flows are stored against; the pixels where
+    the reference's matmul differs from it (none were found) are stored as
+    patches.  tests/test_preprocess.py restates it."""
+    x = np.broadcast_to(np.arange(w, dtype=np.float32)[None, :], (h, w))
+    y = np.broadcast_to(np.arange(h, dtype=np.float32)[:, None], (h, w))
+    dx, dy = (x - c0[0]).astype(np.float32), (y - c0[1]).astype(np.float32)
+    px = (dy.astype(np.float64) * np.float64(rot[1, 0]) + (dx * rot[0, 0]).astype(np.float64)).astype(np.float32)
+    py = (dy.astype(np.float64) * np.float64(rot[1, 1]) + (dx * rot[0, 1]).astype(np.float64)).astype(np.float32)
+    return np.stack(((px + c0[0]) - x, (py + c0[1]) - y)).astype(np.float32)
+
+
+def make_ppa_fill_cases(utils_mod, ref_fw, Convert, h=32, w=40, seeds=(5150, 5151), sample=(5, 7), tol_full=True,
+                        store_flows=False):
     """PreprocessPlusAugment.forward (:329-476) of two 32x40 images with the
     real hole-fill: the reference's text slices run with utils.inpaint backed
     by _Cv2Telea (cv2's sequential Telea, restated by the oracle), the oracle
@@ -509,7 +527,16 @@ def make_ppa_fill_cases(utils_mod, ref_fw, Convert, h=32, w=40, seeds=(5150, 515
 
     ``tol_full=False`` (the larger-image fixture, ppa_fill_large.npz) keeps
     the tolerance channels as a strided sample plus their sum and absolute
-    sum instead of whole planes, so the fixture stays a few MB."""
+    sum instead of whole planes, so the fixture stays a few MB.
+
+    ``store_flows`` (ppa_fill_large.npz) also stores every device-geometry
+    flow the reference drew, exactly: the two ego-motion flows (flow12 of
+    :372, flow03 of :385, whole planes) and each rotation's special / back
+    special flow (:31-41, :63-77) as its rotation matrices and centre plus the
+    pixels where the reference's CPU matmul differs from the float32 numpy
+    base (_rotation_base).  tests/test_preprocess.py feeds them to the product
+    in place of its device geometry: everything downstream must then be bit
+    for bit the reference's (the causal check of the target-index flips)."""
     import tempfile
     import torch.nn as nn
     lines = open(os.path.join(REF, "preprocess.py")).read().split("\n")
@@ -526,6 +553,50 @@ def make_ppa_fill_cases(utils_mod, ref_fw, Convert, h=32, w=40, seeds=(5150, 515
     utils_mod.inpaint = lambda img, valid, coll: ref_inpaint(img.as_subclass(_CpuImage), valid, coll).as_subclass(
         torch.Tensor)
     cases["seeds"] = np.array(seeds)
+    cap = {"ego": [], "rot": []}
+    if store_flows:
+        d2rf = Convert.depth_to_random_flow
+        SF = ns["SpecialFlow"]
+        sf_fwd, sf_rot = SF.forward, SF._rotate
+
+        def cap_d2rf(*a, **k):
+            r = d2rf(*a, **k)
+            cap["ego"].append(r[0].detach().clone())
+            return r
+
+        def cap_rotate(self, size):
+            # the matrices _rotate builds, rebuilt from its own draws: wrap
+            # utils.get_random for the call to see c0 and theta
+            draws = []
+            gr = utils_mod.get_random
+
+            def rec(*a, **k):
+                v = gr(*a, **k)
+                draws.append(v)
+                return v
+            ns_utils = ns["utils"]
+            ns_utils.get_random = rec
+            try:
+                p1, p_prev = sf_rot(self, size)
+            finally:
+                ns_utils.get_random = gr
+            hh, ww = size
+            c0 = torch.tensor((draws[0] + ww / 2, draws[1] + hh / 2)).to(torch.float32)
+            theta = torch.deg2rad(draws[2])
+            rot = torch.tensor([[torch.cos(theta), -torch.sin(theta)], [torch.sin(theta), torch.cos(theta)]]
+                               ).type(torch.float32)
+            rrot = torch.tensor([[torch.cos(-theta), -torch.sin(-theta)], [torch.sin(-theta), torch.cos(-theta)]]
+                                ).type(torch.float32)
+            cap["rot"].append({"c0": c0.numpy(), "rot": rot.numpy(), "rrot": rrot.numpy()})
+            return p1, p_prev
+
+        def cap_fwd(self, size, kind):
+            r = sf_fwd(self, size, kind)
+            if 6. <= kind < 7.:
+                cap["rot"][-1]["flows"] = (r[0].detach().numpy().copy(), r[1].detach().numpy().copy())
+            return r
+        Convert.depth_to_random_flow = staticmethod(cap_d2rf)
+        SF._rotate, SF.forward = cap_rotate, cap_fwd
     for n, seed in enumerate(seeds):
         raw = synth_depth(h, w, seed)
         img0 = torch.from_numpy(synth_rgb(h, w, seed))
@@ -545,6 +616,25 @@ def make_ppa_fill_cases(utils_mod, ref_fw, Convert, h=32, w=40, seeds=(5150, 515
                         z = np.load(os.path.join(out, f"{g}_{a}_{k}.npz"))
                         files[f"{g}_{a}_{k}"] = (z["img_depth_flow"], int(z["augment_flow_type"]))
         cases[f"i{n}/holes"] = np.array([c[0] for c in tel.calls], np.int64)
+        if store_flows:
+            # the reference draws flow12 (:372) before flow03 (:385)
+            assert len(cap["ego"]) == 2 and len(cap["rot"]) == 15, (len(cap["ego"]), len(cap["rot"]))
+            cases[f"i{n}/ref_flow12"] = cap["ego"][0].numpy().astype(np.float32)
+            cases[f"i{n}/ref_flow03"] = cap["ego"][1].numpy().astype(np.float32)
+            for r, rc in enumerate(cap["rot"]):
+                pre = f"i{n}/rot{r}"
+                cases[pre + "/c0"], cases[pre + "/rot"], cases[pre + "/rrot"] = rc["c0"], rc["rot"], rc["rrot"]
+                for nm, m, flow in (("sf", rc["rot"], rc["flows"][0]), ("bsf", rc["rrot"], rc["flows"][1])):
+                    base = _rotation_base(m, rc["c0"], h, w)
+                    assert flow.dtype == np.float32 and flow.shape == base.shape
+                    idx = np.flatnonzero(base.view(np.uint32) != flow.view(np.uint32)).astype(np.int32)
+                    cases[f"{pre}/{nm}_idx"] = idx
+                    cases[f"{pre}/{nm}_val"] = flow.reshape(-1)[idx]
+            cap["ego"].clear()
+            cap["rot"].clear()
+    if store_flows:
+        Convert.depth_to_random_flow = staticmethod(d2rf)
+        SF._rotate, SF.forward = sf_rot, sf_fwd
         for key, (arr, kind) in files.items():
             pre = f"i{n}/{key}"
             cases[pre + "/dtype"] = np.array(arr.dtype.str)
@@ -621,7 +711,7 @@ def main():
         return
     if sys.argv[1:] == ["ppa_fill_large"]:  # one 192x256 image: ego-motion border bands, larger fills
         pf = make_ppa_fill_cases(utils_mod, ref_fw, Convert, h=192, w=256, seeds=(5160,), sample=(8, 8),
-                                 tol_full=False)
+                                 tol_full=False, store_flows=True)
         np.savez_compressed(os.path.join(HERE, "ppa_fill_large.npz"), **pf)
         print("ppa_fill_large.npz", os.path.getsize(os.path.join(HERE, "ppa_fill_large.npz")), "bytes")
         return

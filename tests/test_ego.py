@@ -5,15 +5,15 @@ geometry.BackprojectDepth / Project3D (geometry.py:17-67), and the first
 stage's ego-motion warps (preprocess.py:371-373, :385-387).
 
 Parity bar:
-* the flow plane (ops.ego_flow) equals the reference's to float32 rounding:
-  the two matrix products' accumulation order is torch's GEMM's, which is not
-  specified, so the bar is a tolerance -- |d flow| <= 8 ulp of
+* the flow plane (ops.ego_flow) equals the reference's own runs bit for bit
+  (tests/golden/pipeline.npz, ppa_fill_large.npz: since round 5 P = K @ T is
+  multiplied on the host in the reference's shapes);
+* against this repo's torch restatement evaluated on the GPU (torch's device
+  GEMMs round differently) the bar stays a tolerance -- |d flow| <= 8 ulp of
   max(|p1|, size - 1) per axis (TOL_ULP below; p1 is computed in the
   normalised [-1, 1] domain and scaled by (size - 1) / 2, so its rounding
   error is set by the image size, not by |p1|: 9.5e-6 at 60x80, ~6e-5 at
-  768x1024, where 1 ulp of 1023 is 6.1e-5), checked against the reference's
-  own flows (tests/golden/pipeline.npz flow03, generated by the reference's
-  code) and against this repo's torch restatement on the GPU;
+  768x1024, where 1 ulp of 1023 is 6.1e-5);
 * the fused warp (ops.warp_ego) is bit-identical to FW on ops.ego_flow's plane
   (one device function computes the flow for both);
 * against FW on the reference-arithmetic flow, the targets whose truncated
@@ -47,7 +47,10 @@ def _golden():
 @pytest.mark.gpu
 @pytest.mark.parametrize("img", ["img0", "img1"])
 def test_ego_flow_vs_reference_fixture(img):
-    """flow03 of the golden pipeline: the reference's own code on float32 depth."""
+    """flow03 of the golden pipeline, the reference's own code on float32
+    depth: bit for bit (round 5: P = K @ T multiplied on the host in the
+    reference's shapes, synth.projection; the per-pixel sequence -- k-order
+    fused multiply-adds, IEEE divisions -- is the reference's CPU rounding)."""
     from opticalflowfromdepth_amd import ego_flow, synth
     g = _golden()
     d = torch.from_numpy(g[f"{img}/norm_depth"]).float()[None]  # preprocess.py:385 passes float32 here
@@ -56,8 +59,24 @@ def test_ego_flow_vs_reference_fixture(img):
     P, ik = synth.projection(h, w, torch.from_numpy(g[f"{img}/T1"]), dev)
     got = ego_flow(d.to(dev), P, ik)[0].cpu().numpy()
     ref = g[f"{img}/flow03"]
-    err = np.abs(got - ref)
-    assert (err <= _tol(ref, h, w)).all(), float(err.max())
+    assert np.array_equal(got, ref), int((got != ref).sum())
+
+
+@pytest.mark.gpu
+def test_ego_flow_float64_depth_vs_reference_run():
+    """flow03 of the 192x256 pipeline fixture (preprocess.py:385 on the
+    float64 normalised depth, the reference's run, ppa_fill_large.npz): bit
+    for bit."""
+    from opticalflowfromdepth_amd import ego_flow, synth
+    z = np.load(os.path.join(REPO, "tests", "golden", "ppa_fill_large.npz"))
+    h, w = int(z["h"]), int(z["w"])
+    _, T = synth.camera_params(int(z["seeds"][0]))
+    d0 = synth.normalize_depth(torch.from_numpy(z["i0/raw_depth"].copy())[None, None])
+    assert d0.dtype == torch.float64
+    dev = torch.device("cuda:0")
+    P, ik = synth.projection(h, w, T[None], dev)
+    got = ego_flow(d0.to(dev), P, ik)[0].cpu().numpy()
+    assert np.array_equal(got, z["i0/ref_flow03"]), int((got != z["i0/ref_flow03"]).sum())
 
 
 @pytest.mark.gpu

@@ -21,7 +21,6 @@ from conftest import REPO
 from oracle import oracle
 
 G = np.load(os.path.join(REPO, "tests", "golden", "augment.npz"))
-FLOW_RTOL, FLOW_ATOL = 1e-5, 1e-4  # pixel units
 
 
 def _in(k):
@@ -38,12 +37,10 @@ def test_special_flows_match_reference_geometry(kind):
     p = pp.draw_augment_params(kind, h, w)
     sf, bsf = pp.special_flow_from_params(h, w, kind, None if kind == 5 else (p.view(1, -1) if kind == 6 else p.view(1)),
                                           "cpu")
-    if kind == 5:
-        assert np.array_equal(sf[0].numpy(), G[f"aug{kind}/special"])
-        assert np.array_equal(bsf[0].numpy(), G[f"aug{kind}/back_special"])
-    else:
-        np.testing.assert_allclose(sf[0].numpy(), G[f"aug{kind}/special"], rtol=FLOW_RTOL, atol=FLOW_ATOL)
-        np.testing.assert_allclose(bsf[0].numpy(), G[f"aug{kind}/back_special"], rtol=FLOW_RTOL, atol=FLOW_ATOL)
+    # bit-exact for every kind: the rotation's host path is the reference's
+    # own matmul in its shapes (round 5; a 1e-5 tolerance before)
+    assert np.array_equal(sf[0].numpy(), G[f"aug{kind}/special"])
+    assert np.array_equal(bsf[0].numpy(), G[f"aug{kind}/back_special"])
 
 
 def test_special_flow_module_state_and_draws():
@@ -169,15 +166,17 @@ def test_augment_flow_matches_reference(kind):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind", [6, 7])
-def test_special_flows_on_device_close_to_reference(kind):
+def test_special_flows_on_device_match_reference(kind):
+    """The rotation (ops.rotation_flow: the reference's matmul rounding) and
+    shear flows on the device, bit for bit the reference's."""
     from opticalflowfromdepth_amd import preprocess as pp
     from opticalflowfromdepth_amd import utils
     h, w = G["in/img0"].shape[-2:]
     utils.set_seed(int(G[f"aug{kind}/seed"]))
     p = pp.draw_augment_params(kind, h, w)
     sf, bsf = pp.special_flow_from_params(h, w, kind, p.view(1, -1) if kind == 6 else p.view(1), "cuda:0")
-    np.testing.assert_allclose(sf[0].cpu().numpy(), G[f"aug{kind}/special"], rtol=FLOW_RTOL, atol=FLOW_ATOL)
-    np.testing.assert_allclose(bsf[0].cpu().numpy(), G[f"aug{kind}/back_special"], rtol=FLOW_RTOL, atol=FLOW_ATOL)
+    assert np.array_equal(sf[0].cpu().numpy(), G[f"aug{kind}/special"])
+    assert np.array_equal(bsf[0].cpu().numpy(), G[f"aug{kind}/back_special"])
 
 
 def _cast_only(img, valid, coll):
@@ -187,26 +186,16 @@ def _cast_only(img, valid, coll):
     return torch.from_numpy(a).to(img.device).permute(0, 3, 1, 2).to(torch.float32).contiguous()
 
 
-# group.npz channels (layout preprocess.py:437-440) whose values pass through the
-# ego-motion geometry evaluated on the device (:372-387 with geometry.py:17-67):
-# flow12 / back_flow12 28:32, flow02 / back_flow02p 32:36, flow03 / back_flow03
-# 36:40, flow13 / back_flow13p 40:44 -- all flows; the images and depths 0:24 and
-# the disparity flows 24:28 are exact
-GEOMETRY_GROUP_CH = tuple(range(28, 44))
-GEOMETRY_ATOL = 1e-5  # px: the north_star's fp32 flow tolerance for device geometry
-
-
 def _check_group(got, exp):
-    """Bit-exact on every channel except the device-geometry flows, which are
-    held to GEOMETRY_ATOL; image and depth channels are exact everywhere, so a
-    z-buffer winner that flipped on a last-ulp flow difference would fail."""
+    """Every one of the 44 channels bit for bit, the device-geometry flows
+    included (flow12 / back_flow12 28:32, flow02 / back_flow02p 32:36, flow03 /
+    back_flow03 36:40, flow13 / back_flow13p 40:44): since round 5 the ego-motion
+    flow is the reference's exactly (P = K @ T multiplied on the host in the
+    reference's shapes, synth.projection; before, a 1e-5 px tolerance)."""
     # float64, like the reference's (its get_depth returns float64 and torch.cat promotes)
     assert got.shape == exp.shape == (44,) + exp.shape[1:] and got.dtype == exp.dtype == np.float64
     for c in range(44):
-        if c in GEOMETRY_GROUP_CH:
-            np.testing.assert_allclose(got[c], exp[c], rtol=0, atol=GEOMETRY_ATOL, err_msg=f"group ch {c}")
-        else:
-            assert np.array_equal(got[c], exp[c]), f"group ch {c}: {(got[c] != exp[c]).sum()} px differ"
+        assert np.array_equal(got[c], exp[c]), f"group ch {c}: {(got[c] != exp[c]).sum()} px differ"
 
 
 @pytest.mark.gpu
@@ -229,11 +218,9 @@ def test_forward_all_files_match_reference(tmp_path, workers):
     group.npz and the 120 {g}_{a}_{1,2}.npz), read back with np.load; with the
     synchronous writer and with the NpzWriter thread pool.
 
-    Tolerance: images, depths and augment_flow_type bit-exact in all 121
-    files; flows bit-exact except where they pass through geometry evaluated
-    on the device -- the group's ego-motion channels and the rotation
-    augmentations (type 6, cos / sin of preprocess.py:66-75) -- held to
-    1e-5 px.  The test also counts the files that are entirely bit-exact."""
+    Bar: all 121 files bit for bit, every channel -- images, depths, flows
+    (the device's ego-motion and rotation geometry included) and
+    augment_flow_type."""
     from opticalflowfromdepth_amd import preprocess as pp, utils
     z = np.load(os.path.join(REPO, "tests", "golden", "ppa_forward.npz"))
     ppa = pp.PreprocessPlusAugment("cuda:0", inpaint_fn=_cast_only, writer_workers=workers)
@@ -257,15 +244,10 @@ def test_forward_all_files_match_reference(tmp_path, workers):
                 # float64 or float32 by kind, like the reference's (the special flows are float32)
                 assert got.shape == exp.shape == (8,) + exp.shape[1:] and got.dtype == exp.dtype, key
                 # data1 = (img1, img1_depth, flow, back_flow), data2 = (flow, back_flow, img2, img2_depth)
-                flow_ch = (4, 5, 6, 7) if k == 1 else (0, 1, 2, 3)
                 for c in range(8):
-                    if c in flow_ch and kind == 6:
-                        np.testing.assert_allclose(got[c], exp[c], rtol=0, atol=GEOMETRY_ATOL, err_msg=f"{key} c{c}")
-                    else:
-                        assert np.array_equal(got[c], exp[c]), f"{key} c{c}: {(got[c] != exp[c]).sum()} px differ"
+                    assert np.array_equal(got[c], exp[c]), f"{key} c{c}: {(got[c] != exp[c]).sum()} px differ"
                 exact_files += bool(np.array_equal(got, exp))
-    # every non-rotation file (90 of 120) is bit-exact
-    assert exact_files >= 90, exact_files
+    assert exact_files == 120, exact_files
 
 
 # ---------------------------------------------------------------- the real fill, end to end
@@ -279,87 +261,59 @@ def _digest(a) -> str:
     return f"{a.dtype.str}{tuple(a.shape)}:" + hashlib.sha256(a.tobytes()).hexdigest()
 
 
-FLIP_FRAC_MAX = 0.02  # of a channel's sampled pixels, larger fixture only
-
-
-def _check_file_vs_fill_fixture(z, pre, arr, kind=None, flips=None):
-    """One written array vs tests/golden/ppa_fill.npz: dtype and shape as the
-    reference's; every channel bit-exact (SHA-256 digest) except the
-    device-geometry flows (the group's ego-motion channels, the rotation
-    augmentations' flows), held to GEOMETRY_ATOL against the stored values."""
+def _check_file_vs_fill_fixture(z, pre, arr, kind=None):
+    """One written array vs a fill fixture (ppa_fill.npz / ppa_fill_large.npz):
+    dtype and shape as the reference's, every channel bit-exact (SHA-256
+    digest of the reference's channel).  The device-geometry flows included:
+    since round 5 the product's ego-motion and rotation flows are the
+    reference's bit for bit, so no channel needs a tolerance or a flip budget."""
     assert arr.dtype.str == str(z[pre + "/dtype"]) and arr.shape == tuple(z[pre + "/shape"]), pre
     if kind is not None:
         assert kind == int(z[pre + "/type"]), pre
     dig = z[pre + "/digest"]
     sy, sx = (int(v) for v in z["sample_stride"]) if "sample_stride" in z.files else (5, 7)
-    geometry_file = any(f"{pre}/tolsum{c}" in z.files for c in range(arr.shape[0]))
-    exact = True
     for c in range(arr.shape[0]):
-        tol, tolsum = f"{pre}/tol{c}", f"{pre}/tolsum{c}"
-        if tol in z.files:
-            np.testing.assert_allclose(arr[c], z[tol].astype(arr.dtype), rtol=0, atol=GEOMETRY_ATOL,
-                                       err_msg=f"{pre} c{c}")
-            exact &= _digest(arr[c]) == str(dig[c])
-        elif tolsum in z.files:
-            # larger fixture: the strided sample within the tolerance, and the
-            # plane's sum and absolute sum within (pixels x tolerance).  The
-            # tolerance is the ego-flow module's bar (tests/test_ego.py): 8 ulp
-            # of the image's extent, as float32 flows near 255 px carry ulps of
-            # 1.5e-5 (1e-5 absolute stays the 32x40 images' bar)
-            atol = max(GEOMETRY_ATOL, 8 * float(np.spacing(np.float32(max(arr.shape[-2:]) - 1))))
-            got, samp = arr[c, ::sy, ::sx], z[pre + "/sample"][c].astype(arr.dtype)
-            allow = 0.0
-            if flips is not None:
-                # the flows of a file warped along a device-geometry flow flip
-                # with its image channels (below): sampled pixels beyond the
-                # tolerance counted as flips, the sums allowed that many pixels
-                bad = np.abs(got.astype(np.float64) - samp) > atol
-                if bad.any():
-                    assert bad.mean() <= FLIP_FRAC_MAX, (pre, c, float(bad.mean()))
-                    flips.append((pre, c, float(bad.mean())))
-                allow = FLIP_FRAC_MAX * arr[c].size * float(np.abs(samp).max(initial=0.0))
-            else:
-                np.testing.assert_allclose(got, samp, rtol=0, atol=atol, err_msg=f"{pre} c{c} sample")
-            a64 = arr[c].astype(np.float64)
-            ref_sum, ref_abs = (float(v) for v in z[tolsum])
-            assert abs(a64.sum() - ref_sum) <= a64.size * atol + allow, (pre, c)
-            assert abs(np.abs(a64).sum() - ref_abs) <= a64.size * atol + allow, (pre, c)
-            exact &= _digest(arr[c]) == str(dig[c])
-        else:
-            if _digest(arr[c]) != str(dig[c]):
-                samp = z[pre + "/sample"][c]
-                got = arr[c, ::sy, ::sx]
-                if geometry_file and flips is not None:
-                    # warped along a device-geometry flow: a target index may
-                    # flip where the flow sits within rounding of an integer
-                    # (SURVEY 8f row 1) -- counted, and bounded
-                    frac = float((got != samp.astype(arr.dtype)).mean())
-                    assert frac <= FLIP_FRAC_MAX, (pre, c, frac)
-                    flips.append((pre, c, frac))
-                    exact = False
-                    continue
-                raise AssertionError(f"{pre} c{c} differs; sample got {got.ravel()[:6]} exp {samp.ravel()[:6]}")
-    return exact
+        if _digest(arr[c]) != str(dig[c]):
+            samp = z[pre + "/sample"][c]
+            got = arr[c, ::sy, ::sx]
+            nd = int((got != samp.astype(arr.dtype)).sum())
+            raise AssertionError(f"{pre} c{c} differs ({nd} of {samp.size} sampled pixels); "
+                                 f"sample got {got.ravel()[:6]} exp {samp.ravel()[:6]}")
 
 
-def _check_dir_vs_fill_fixture(z, n, out, flips=None):
+def _check_dir_vs_fill_fixture(z, n, out):
     from opticalflowfromdepth_amd import preprocess as pp
     assert sorted(os.listdir(out)) == sorted(["group.npz"] + [f"{g}_{a}_{k}.npz" for g in range(5)
                                                              for a in range(12) for k in (1, 2)])
-    _check_file_vs_fill_fixture(z, f"i{n}/group", np.load(os.path.join(out, "group.npz"))["img_depth_flow"],
-                                flips=flips)
-    inexact = []
+    _check_file_vs_fill_fixture(z, f"i{n}/group", np.load(os.path.join(out, "group.npz"))["img_depth_flow"])
     for g in range(5):
         for a, kind in enumerate(pp.AUGMENT_SCHEDULE):
             for k in (1, 2):
                 key = f"{g}_{a}_{k}"
                 f = np.load(os.path.join(out, key + ".npz"))
-                if not _check_file_vs_fill_fixture(z, f"i{n}/{key}", f["img_depth_flow"],
-                                                   int(f["augment_flow_type"]), flips):
-                    inexact.append((key, kind))
-    # group 0's flows (disparity flow01 and its back flow) never pass through
-    # device geometry: its non-rotation files are bit-exact whole
-    assert not [key for key, kind in inexact if key.startswith("0_") and kind != 6], inexact
+                _check_file_vs_fill_fixture(z, f"i{n}/{key}", f["img_depth_flow"], int(f["augment_flow_type"]))
+
+
+def _large_fixture():
+    z = np.load(os.path.join(REPO, "tests", "golden", "ppa_fill_large.npz"))
+    assert (int(z["h"]), int(z["w"])) == (192, 256)
+    return z
+
+
+def _run_large(z, out, persist=None):
+    """PreprocessPlusAugment.forward on the large fixture's image into ``out``."""
+    from opticalflowfromdepth_amd import _native, preprocess as pp, utils
+    lib = _native.lib()
+    prev = lib.ofd_fw_set_persist_min(-1)
+    if persist is not None:
+        lib.ofd_fw_set_persist_min(persist)
+    try:
+        ppa = pp.PreprocessPlusAugment("cuda:0")
+        utils.set_seed(int(z["seeds"][0]))
+        ppa((torch.from_numpy(z["i0/img0"]), torch.from_numpy(z["i0/raw_depth"].copy()).unsqueeze(0)), out, False)
+        torch.cuda.synchronize()
+    finally:
+        lib.ofd_fw_set_persist_min(prev)
 
 
 @pytest.mark.gpu
@@ -372,36 +326,89 @@ def test_forward_larger_image_with_the_default_fill_matches_reference(tmp_path, 
     takes the persistent SPLAT (its per-XCD queues and their restore) instead
     of the one-workgroup-per-tile SPLAT this short call picks by default.
     Pins the oracle-Telea pipeline, as the 32x40 case does (see its docstring).
-    At this size an image / depth channel warped along a device-geometry flow
-    (groups 1-4, the rotations) may differ where a flow sits within rounding
-    of an integer and the truncated target flips: such
-    channels are counted and bounded (<= 2 % of the sampled pixels each);
-    every other channel of the 121 files is bit-exact."""
-    from opticalflowfromdepth_amd import _native, preprocess as pp, utils
-    z = np.load(os.path.join(REPO, "tests", "golden", "ppa_fill_large.npz"))
-    assert (int(z["h"]), int(z["w"])) == (192, 256)
-    lib = _native.lib()
-    prev = lib.ofd_fw_set_persist_min(-1)
-    if persist is not None:
-        lib.ofd_fw_set_persist_min(persist)
-    try:
-        ppa = pp.PreprocessPlusAugment("cuda:0")
-        out = str(tmp_path / "img")
-        utils.set_seed(int(z["seeds"][0]))
-        ppa((torch.from_numpy(z["i0/img0"]), torch.from_numpy(z["i0/raw_depth"].copy()).unsqueeze(0)), out, False)
-        torch.cuda.synchronize()
-    finally:
-        lib.ofd_fw_set_persist_min(prev)
+
+    Bar: all 968 channels of the 121 files bit-exact -- no tolerance and no
+    target-index flip budget.  Round 4 allowed up to 120 channels with
+    flipped targets, where the device's ego-motion / rotation flows sat
+    within rounding of an integer; round 5 made those flows the reference's
+    bit for bit (synth.projection, ops.rotation_flow), and every flip went."""
+    z = _large_fixture()
+    out = str(tmp_path / "img")
+    _run_large(z, out, persist)
     assert z["i0/holes"].sum() > 300000
-    flips = []
-    _check_dir_vs_fill_fixture(z, 0, out, flips)
-    # the channels warped along device-geometry flows (groups 1-4, rotations)
-    # may carry target-index flips; every other channel of the 121 files is
-    # bit-exact, and the flips stay rare
-    print(f"target-index flips: {len(flips)} channels of 968, worst {max((f for _, _, f in flips), default=0):.4f}")
-    assert len(flips) <= 120, flips
-    if flips:
-        assert max(f for _, _, f in flips) <= FLIP_FRAC_MAX
+    _check_dir_vs_fill_fixture(z, 0, out)
+
+
+def _reference_rotation(z, r, h, w):
+    """The reference's rotation special / back special flows of rotation r
+    (preprocess.py:63-77), rebuilt from the fixture: the float32 GEMM-rounding
+    base (make_golden.py _rotation_base, restated) plus the stored patches."""
+    x = np.broadcast_to(np.arange(w, dtype=np.float32)[None, :], (h, w))
+    y = np.broadcast_to(np.arange(h, dtype=np.float32)[:, None], (h, w))
+    c0 = z[f"i0/rot{r}/c0"]
+    out = []
+    for nm, m in (("sf", "rot"), ("bsf", "rrot")):
+        R = z[f"i0/rot{r}/{m}"]
+        dx, dy = (x - c0[0]).astype(np.float32), (y - c0[1]).astype(np.float32)
+        px = (dy.astype(np.float64) * np.float64(R[1, 0]) + (dx * R[0, 0]).astype(np.float64)).astype(np.float32)
+        py = (dy.astype(np.float64) * np.float64(R[1, 1]) + (dx * R[0, 1]).astype(np.float64)).astype(np.float32)
+        f = np.stack(((px + c0[0]) - x, (py + c0[1]) - y)).astype(np.float32).reshape(-1)
+        f[z[f"i0/rot{r}/{nm}_idx"]] = z[f"i0/rot{r}/{nm}_val"]
+        out.append(torch.from_numpy(f.reshape(2, h, w)))
+    return out
+
+
+@pytest.mark.gpu
+def test_forward_larger_image_with_the_reference_flows_matches_reference(tmp_path, monkeypatch):
+    """Causal check of the device geometry: the pipeline run with every
+    device-geometry flow replaced by the reference's own (flow03 / flow12 of
+    preprocess.py:372, :385 and the 15 rotation special flows of :63-77, all
+    stored in ppa_fill_large.npz) must write the reference's 121 files bit for
+    bit.  So everything downstream of the flows -- the warps, the composed
+    flows, the fills, the masks, the file layout -- is exact by itself, and
+    the default run's agreement (the test above) is the geometry's."""
+    from opticalflowfromdepth_amd import preprocess as pp
+    z = _large_fixture()
+    h, w = int(z["h"]), int(z["w"])
+    ego = [torch.from_numpy(z["i0/ref_flow03"]), torch.from_numpy(z["i0/ref_flow12"])]  # the product's call order
+    calls = {"ego": 0, "rot": 0}
+
+    def ref_ego(depth, device=None, segment=None, T1=None):
+        f = ego[calls["ego"]].to(depth.device)
+        calls["ego"] += 1
+        return (f[None] if depth.dim() == 4 else f), T1
+
+    orig = pp.special_flow_from_params
+
+    def ref_special(hh, ww, kind, params, device):
+        if kind != 6:
+            return orig(hh, ww, kind, params, device)
+        r = calls["rot"]
+        calls["rot"] += 1
+        assert params.shape[0] == 1 and np.allclose(params[0, :2].numpy(), z[f"i0/rot{r}/c0"])
+        sf, bsf = _reference_rotation(z, r, h, w)
+        return sf[None].to(device), bsf[None].to(device)
+
+    monkeypatch.setattr(pp.Convert, "depth_to_random_flow", staticmethod(ref_ego))
+    monkeypatch.setattr(pp, "special_flow_from_params", ref_special)
+    out = str(tmp_path / "img")
+    _run_large(z, out)
+    assert calls == {"ego": 2, "rot": 15}
+    _check_dir_vs_fill_fixture(z, 0, out)
+
+
+@pytest.mark.gpu
+def test_forward_larger_image_check_catches_a_wrong_ego_motion(tmp_path, monkeypatch):
+    """The bar has teeth: a deliberately wrong ego-motion flow -- T transposed
+    before P = K @ T -- must fail the fixture check."""
+    from opticalflowfromdepth_amd import synth
+    z = _large_fixture()
+    orig = synth.projection
+    monkeypatch.setattr(synth, "projection", lambda h, w, T, device: orig(h, w, T.transpose(-1, -2), device))
+    out = str(tmp_path / "img")
+    _run_large(z, out)
+    with pytest.raises(AssertionError):
+        _check_dir_vs_fill_fixture(z, 0, out)
 
 
 @pytest.mark.gpu
@@ -412,10 +419,8 @@ def test_forward_with_the_default_fill_matches_reference(tmp_path, n):
     the reference's forward (preprocess.py:329-476) wrote when its
     utils.inpaint (utils.py:136-151) ran cv2's Telea as restated by the oracle
     (tests/golden/ppa_fill.npz; 95 fills per image, ~16k pixels filled).
-    Images and depths bit-exact in all 121 files; flows bit-exact except
-    those that pass through the device's ego-motion geometry (the group's
-    channels 28-43, every flow of groups 1-4's augmentations, the rotation
-    augmentations), held to the 1e-5 px geometry tolerance.
+    Every channel of all 121 files bit-exact, the flows that pass through
+    the device's ego-motion and rotation geometry included.
 
     What this pins: the product against the reference's pipeline with the
     ORACLE's Telea (oracle/inpaint_oracle.c sequential mode) standing in for
