@@ -31,10 +31,11 @@
  *   ofd_inpaint_workspace_bytes, ofd_inpaint_seq_workspace_bytes
  *       no reference counterpart (cv2 allocates its fast-marching state per
  *       call); caller-owned scratch, no initialisation needed.
- *   ofd_inpaint_seq_set_groups, ofd_inpaint_seq_helper_device
+ *   ofd_inpaint_seq_set_groups, ofd_inpaint_seq_helper_device, ofd_inpaint_seq_set_pipeline
  *       no reference counterpart: how many stream-parallel groups the
  *       sequential fill splits a batch into (results never depend on it),
- *       and the device whose helper streams a call would use.
+ *       the device whose helper streams a call would use, and the record /
+ *       colour rounds pipelined beside the fast marches.
  *   ofd_inpaint_set_schedule
  *       no reference counterpart: diagnostics / tests only (how many hole
  *       layers are launched one by one before the deep-tail
@@ -101,6 +102,18 @@ int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float 
  * default comes from OFD_SEQ_GROUPS (else 1).  Process-wide;
  * returns the previous setting. */
 int ofd_inpaint_seq_set_groups(int groups);
+
+/* The pipelined sequential fill (radius 3, C <= 3 -- utils.inpaint's call --
+ * on images of at least 2^18 pixels): `rounds` record / colour rounds run on
+ * a helper stream beside the fast marches, each about `round_us` apart, over
+ * the holes the inner march has finished; the final round after the marches
+ * takes the rest.  rounds = 0 runs the record and colour passes after the
+ * marches only.  force = 1 pipelines smaller images too (tests).  Results
+ * never depend on any of it.  Negative values leave a setting as it is;
+ * defaults OFD_SEQ_PIPE (12) and OFD_SEQ_PIPE_US (1200).  Process-wide;
+ * returns the previous number of rounds.  Grouped fills
+ * (ofd_inpaint_seq_set_groups > 1) are not pipelined. */
+int ofd_inpaint_seq_set_pipeline(int rounds, int round_us, int force);
 
 /* The device whose helper streams a grouped sequential fill on `stream`
  * would use: the stream's own device (helpers are kept per device and

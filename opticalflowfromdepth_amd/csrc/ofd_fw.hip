@@ -467,7 +467,9 @@ struct EgoCoords {
 template <typename F, typename D>
 struct FlowCatCoords {
     using V = F;
-    static constexpr int kGen = 3, kGenGT = 8;
+    // targets in flight per publish thread: every target's two flow gathers
+    // stay live until the stores, so float64 flows keep 4 (8 spilled)
+    static constexpr int kGen = 3, kGenGT = sizeof(F) == 8 ? 4 : 8;
     static constexpr bool kPackable = true;
     const F *flow;   // [B,2,H,W]
     const D *depth;  // [B,1,H,W]
@@ -514,6 +516,23 @@ struct FlowCatCoords {
         g[1] = float(f[0] * F(-1.0));
         g[2] = float(f[HW] * F(-1.0));
     }
+    // The publish's split form (kGenSplit): gen_vals has no branch and no
+    // store, so a thread issues every target's flow gathers before its first
+    // output store (gen_key's per-target loads, each behind the previous
+    // target's stores, serialised the publish: 683 vs ~640 us per 64 images
+    // of the plain FW on the same flows); the depth channel comes from the
+    // key, and gen_fix rewrites the rare winner whose key decodes to 0 (the
+    // depth plane holds the sign the key folded).
+    static constexpr bool kGenSplit = true;
+    __device__ __forceinline__ void gen_vals(int64_t b, unsigned w, unsigned long long key, float g[3]) const {
+        const F *f = flow + b * 2 * HW + w;
+        g[0] = depth_from_key(key);
+        g[1] = float(f[0] * F(-1.0));
+        g[2] = float(f[HW] * F(-1.0));
+    }
+    __device__ __forceinline__ void gen_fix(int64_t b, unsigned w, unsigned long long key, float *dst) const {
+        if (depth_from_key(key) == 0.0f) __builtin_nontemporal_store(float(depth[b * HW + w]), dst);
+    }
     __host__ bool vec_ok() const { return (uintptr_t(flow) | uintptr_t(depth)) % 16 == 0; }
     __device__ __forceinline__ void target(int64_t, int i, int j, V x, V y, int H, int W, int &tx, int &ty) const {
         target_flow<F>(i, j, x, y, H, W, tx, ty);
@@ -543,6 +562,11 @@ __global__ __launch_bounds__(256) void ego_flow_kernel(EgoCoords<D> co, float *_
         fyp[i] = fy;
     }
 }
+
+template <typename C, typename = void>
+struct GenSplit : std::false_type {};
+template <typename C>
+struct GenSplit<C, std::void_t<decltype(C::kGenSplit)>> : std::integral_constant<bool, C::kGenSplit> {};
 
 // ---------------------------------------------------------------- wave helpers
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
@@ -1257,16 +1281,30 @@ __device__ __forceinline__ void splat_tile(TileLds &L, unsigned lin, int bl, int
                     for (int cc = 0; cc < kCh; ++cc)
                         o[u][cc] = (w[u] != WIN_NONE && c0 + cc < Cobj) ? ob[unsigned(c0 + cc) * uHW + w[u]] : 0.f;
                 if (c0 == 0) {  // the generated channels, computed while the first gathers fly
+                    if constexpr (GenSplit<Coords>::value) {
+                        // every target's gathers first, then the stores
+                        float g[kT][kG];
 #pragma unroll
-                    for (int u = 0; u < kT; ++u) {
-                        float g[kG];
+                        for (int u = 0; u < kT; ++u) co.gen_vals(b, w[u] != WIN_NONE ? w[u] : 0u, kk[u], g[u]);
 #pragma unroll
-                        for (int e = 0; e < kG; ++e) g[e] = 0.f;
-                        if (w[u] != WIN_NONE) co.gen_key(b, w[u], kk[u], g);
-                        if (in[u])
+                        for (int u = 0; u < kT; ++u)
+                            if (in[u])
 #pragma unroll
-                            for (int e = 0; e < kG; ++e)
-                                __builtin_nontemporal_store(g[e], oo + unsigned(ga + e) * uHW + t[u]);
+                                for (int e = 0; e < kG; ++e)
+                                    __builtin_nontemporal_store(w[u] != WIN_NONE ? g[u][e] : 0.f,
+                                                                oo + unsigned(ga + e) * uHW + t[u]);
+                    } else {
+#pragma unroll
+                        for (int u = 0; u < kT; ++u) {
+                            float g[kG];
+#pragma unroll
+                            for (int e = 0; e < kG; ++e) g[e] = 0.f;
+                            if (w[u] != WIN_NONE) co.gen_key(b, w[u], kk[u], g);
+                            if (in[u])
+#pragma unroll
+                                for (int e = 0; e < kG; ++e)
+                                    __builtin_nontemporal_store(g[e], oo + unsigned(ga + e) * uHW + t[u]);
+                        }
                     }
                 }
 #pragma unroll
@@ -1277,6 +1315,13 @@ __device__ __forceinline__ void splat_tile(TileLds &L, unsigned lin, int bl, int
                         if (in[u] && c < Cobj)
                             __builtin_nontemporal_store(o[u][cc], oo + unsigned(c < ga ? c : c + kG) * uHW + t[u]);
                     }
+            }
+            if constexpr (GenSplit<Coords>::value) {
+                // the rare winner whose key decodes to a zero depth: its sign
+                // from the depth plane (after this thread's stores: same address)
+#pragma unroll
+                for (int u = 0; u < kT; ++u)
+                    if (in[u] && w[u] != WIN_NONE) co.gen_fix(b, w[u], kk[u], oo + unsigned(ga) * uHW + t[u]);
             }
         }
     } else if constexpr (kFuse) {

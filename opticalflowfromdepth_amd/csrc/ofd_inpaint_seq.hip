@@ -109,16 +109,44 @@ struct SqWs {
     uint32_t *meta;  // kMeta words per image
     uint32_t *rec;   // radius-3 COLOUR: kRecW words per hole, indexed by padded pixel
     uint32_t *shd;   // radius-3 COLOUR: the image as packed uint8 channels (C <= 3), H x W words
-    uint64_t *fr2;   // radius-3 COLOUR: second frontier buffer (entries beyond the LDS capacity)
+    uint64_t *fr2;   // radius-3 COLOUR: frontier buffers (entries beyond the LDS capacity)
+    uint64_t *fr3;
+    uint32_t *olog;  // outer march: push log (en), its T (en), sort buffers (2 x 2 en)
+    uint32_t *rpx;   // large buckets' pops by rank: inner (en), outer (en)
+    uint32_t *kc;    // radius-3 COLOUR: Kahn counters (kK - earlier holes, + 1 per release)
+    uint64_t *rq;    // radius-3 COLOUR: holes RECORD found ready (pixel << 32 | pixel)
+    uint32_t *pipe;  // kPipe words per image: pipelined fill control (kP* below)
     int64_t en, eh, ew, hw;
 };
+
+// Pipelined fill control words (per image, kPipe words = two 128-byte lines
+// apart from meta): the march publishes the first line, the pacing kernel
+// owns the second (different writers never share a cache line).
+constexpr int kPipe = 64;
+constexpr int kPProg = 0;      // inner march: log entries [0, prog) final (release-published)
+constexpr int kPOutDone = 1;   // outer march done (its distances negated), release-published
+constexpr int kPInDone = 2;    // inner march done
+constexpr int kPRecDone = 32;  // holes of stamp < recdone recorded
+constexpr int kPLo = 33, kPHi = 34;  // the current RECORD window of stamps [lo, hi)
+constexpr int kPRqc = 35;      // ready-queue entries COLOUR3 has consumed
+constexpr int kPT0 = 36;       // image 0: the pacing clock origin (2 words)
+// timeline (constant-rate clock, 2 words each; tools/seq_time.py): FMM start,
+// outer march end, inner march end (march's line); first and last COLOUR3
+// round with work, rounds with work (pacing line)
+constexpr int kPTFmm = 8, kPTOut = 10, kPTIn = 12, kPTc0 = 40, kPTc1 = 42, kPCRounds = 44;
+__device__ __forceinline__ void put64(uint32_t *p, uint64_t v) {
+    p[0] = uint32_t(v);
+    p[1] = uint32_t(v >> 32);
+}
+constexpr uint32_t kK = 64;    // a hole is ready when its counter reaches kK (> 60 earlier holes)
 
 constexpr int kRecW = 40;  // record words: 32 weights (lane-major), 4 code words, dependants mask (2), weight sum, pad
 
 size_t per_image_bytes(int64_t H, int64_t W) {
     const size_t en = size_t(H + 2) * size_t(W + 2);
     return align256(en * 4) * 6 + align256(en * 8) * 2 + align256(size_t(H + 2) * 4) + kMeta * 4 +
-           en * kRecW * 4 + size_t(H) * size_t(W) * 4 + en * 8 + 3 * 256;
+           en * kRecW * 4 + size_t(H) * size_t(W) * 4 + en * 8 + 3 * 256 +
+           en * 8 + en * 4 * 6 + en * 4 * 2 + en * 4 + en * 8 + kPipe * 4 + 6 * 256;
 }
 
 SqWs carve(void *ws, int64_t G, int64_t H, int64_t W) {
@@ -141,15 +169,21 @@ SqWs carve(void *ws, int64_t G, int64_t H, int64_t W) {
     w.hw = H * W;
     w.rec = reinterpret_cast<uint32_t *>(p), p += align256(size_t(G) * size_t(w.en) * kRecW * 4);
     w.shd = reinterpret_cast<uint32_t *>(p), p += align256(size_t(G) * size_t(w.hw) * 4);
-    w.fr2 = reinterpret_cast<uint64_t *>(p);
+    w.fr2 = reinterpret_cast<uint64_t *>(p), p += align256(size_t(G) * size_t(w.en) * 8);
+    w.fr3 = reinterpret_cast<uint64_t *>(p), p += align256(size_t(G) * size_t(w.en) * 8);
+    w.olog = reinterpret_cast<uint32_t *>(p), p += align256(size_t(G) * size_t(w.en) * 4 * 6);
+    w.rpx = reinterpret_cast<uint32_t *>(p), p += align256(size_t(G) * size_t(w.en) * 4 * 2);
+    w.kc = reinterpret_cast<uint32_t *>(p), p += align256(size_t(G) * size_t(w.en) * 4);
+    w.rq = reinterpret_cast<uint64_t *>(p), p += align256(size_t(G) * size_t(w.en) * 8);
+    w.pipe = reinterpret_cast<uint32_t *>(p);
     return w;
 }
 
 // One image's view of the workspace
 struct Img {
-    uint32_t *sO, *sI, *own, *logp, *rowc, *meta, *rec, *shd;
+    uint32_t *sO, *sI, *own, *logp, *rowc, *meta, *rec, *shd, *olog, *rpx, *kc, *pipe;
     float *t, *logt;
-    uint64_t *k0, *k1, *fr2;
+    uint64_t *k0, *k1, *fr2, *fr3, *rq;
     int64_t en;
     int eh, ew;
 };
@@ -169,6 +203,12 @@ __device__ __forceinline__ Img image(const SqWs &w, int64_t bl) {
     m.rec = w.rec + bl * w.en * kRecW;
     m.shd = w.shd + bl * w.hw;
     m.fr2 = w.fr2 + bl * w.en;
+    m.fr3 = w.fr3 + bl * w.en;
+    m.olog = w.olog + bl * w.en * 6;
+    m.rpx = w.rpx + bl * w.en * 2;
+    m.kc = w.kc + bl * w.en;
+    m.rq = w.rq + bl * w.en;
+    m.pipe = w.pipe + bl * kPipe;
     m.en = w.en;
     m.eh = int(w.eh);
     m.ew = int(w.ew);
@@ -317,6 +357,7 @@ __global__ __launch_bounds__(256) void sq_init_kernel(SqWs w, int range) {
             m.sO[p] = ring ? INF : 0u;
             m.t[p] = band ? 0.f : T_FAR;
             m.own[p] = INF;
+            m.kc[p] = 0u;
         }
         nband += __popcll(__ballot(band));
     }
@@ -373,6 +414,7 @@ __global__ __launch_bounds__(256) void sq_init_tile_kernel(SqWs w, int range) {
             m.sO[p] = ring ? INF : 0u;
             m.t[p] = band ? 0.f : T_FAR;
             m.own[p] = INF;
+            m.kc[p] = 0u;
         }
         const unsigned nb = unsigned(__popcll(__ballot(band)));
         if (lane == 0 && nb) atomicAdd(&m.rowc[i], nb);
@@ -395,6 +437,7 @@ __global__ __launch_bounds__(kThreads) void sq_band_scan_kernel(SqWs w) {
     if (threadIdx.x == 0) {
         for (int k = 0; k < kMeta; ++k) m.meta[k] = 0u;
         m.meta[0] = carry;
+        for (int k = 0; k < kPipe; ++k) m.pipe[k] = 0u;
     }
 }
 
@@ -413,8 +456,8 @@ __global__ __launch_bounds__(256) void sq_band_write_kernel(SqWs w) {
             const uint32_t s = off + __popcll(bal & ((uint64_t(1) << lane) - 1));
             m.logp[s] = uint32_t(p);
             m.logt[s] = 0.f;
-            m.rec[s] = uint32_t(p);  // the outer march's log (outer_view)
-            reinterpret_cast<float *>(m.rec + m.en)[s] = 0.f;
+            m.olog[s] = uint32_t(p);  // the outer march's log (outer_view)
+            reinterpret_cast<float *>(m.olog + m.en)[s] = 0.f;
         }
         off += __popcll(bal);
     }
@@ -706,10 +749,26 @@ constexpr int kFB = OFD_FMM_B;
 // pixels whose stamp is INF, starting from the band in log[0, nb).  Leaves
 // every push's stamp, distance and log entry; returns the number of log
 // entries (band + pushes).
+// Pipelined fill: the inner march publishes how far its log is final (the
+// entries of completed buckets) at most every kPubTicks of the constant-rate
+// clock, for the record / colour rounds running beside it.  Called by every
+// thread right after a workgroup barrier that followed the bucket's stores:
+// thread 0's agent-scope release store then carries every thread's stores
+// (each waited for its own before the barrier).
+constexpr uint64_t kPubTicks = 10000;  // 100 us at 100 MHz
+__device__ __forceinline__ void publish_prog(const Img &m, uint32_t seq, uint64_t &last, bool force) {
+    if (threadIdx.x != 0) return;
+    const uint64_t now = wall_clock64();
+    if (!force && now - last < kPubTicks) return;
+    last = now;
+    __hip_atomic_store(&m.pipe[kPProg], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <bool kInner>
 __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L, uint32_t &nbuckets, uint64_t *prof,
-                         double bscale) {
+                         double bscale, bool pub = false) {
     (void)prof;
+    uint64_t last_pub = 0;
     const int tid = threadIdx.x, ew = m.ew;
     const int64_t off[4] = {-int64_t(ew), -1, int64_t(ew), 1};  // cv2's q = 0..3: up, left, down, right
     uint32_t seq = nb;
@@ -799,7 +858,7 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
             // the counting sort also lays the pops' pixels out by rank (the
             // claims and pushes of these long buckets then skip one dependent
             // load per pop); the area is free until RECORD
-            uint32_t *rank_px = m.rec + (kInner ? 7 : 6) * m.en;
+            uint32_t *rank_px = m.rpx + (kInner ? 0 : m.en);
             if (uniform)
                 keys = m.k0;
             else if (digit_sort(m.k0, m.k1, n, L, m.logp, rank_px)) {
@@ -958,6 +1017,7 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
             SQ_ACC(pb + 4, f4, f5a);
             seq += npush;
             sync_all();
+            if (kInner && pub) publish_prog(m, seq, last_pub, false);
             SQ_T(f6a);
             SQ_ACC(pb + 5, f5a, f6a);
 #ifdef OFD_BUCKET_TRACE
@@ -1037,6 +1097,7 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
         for (uint32_t i = tid; i < npush; i += kThreads) m.logt[seq + i] = m.t[m.logp[seq + i]];
         seq += npush;
         sync_all();
+        if (kInner && pub) publish_prog(m, seq, last_pub, false);
         SQ_T(f6);
         SQ_ACC(pb + 5, f5, f6);
 #ifdef OFD_BUCKET_TRACE
@@ -1057,13 +1118,13 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
     return seq;
 }
 
-// The outer march's push log and sort buffers: the record area, which is
-// free until RECORD (24 of its 160 bytes per padded pixel).
+// The outer march's push log and sort buffers (its own area: the pipelined
+// fill records holes while the marches run).
 __device__ __forceinline__ Img outer_view(const Img &m) {
     Img o = m;
-    o.logp = m.rec;
-    o.logt = reinterpret_cast<float *>(m.rec + m.en);
-    o.k0 = reinterpret_cast<uint64_t *>(m.rec + 2 * m.en);
+    o.logp = m.olog;
+    o.logt = reinterpret_cast<float *>(m.olog + m.en);
+    o.k0 = reinterpret_cast<uint64_t *>(m.olog + 2 * m.en);
     o.k1 = o.k0 + m.en;
     return o;
 }
@@ -1074,7 +1135,7 @@ __device__ __forceinline__ Img outer_view(const Img &m) {
 // They touch disjoint pixels (ring pixels are not 4-adjacent to holes) and
 // keep separate stamps, logs and sort buffers; the only value both read is
 // the band's zero distance (band_t).
-__global__ __launch_bounds__(kThreads) void sq_fmm_kernel(SqWs w, double bscale) {
+__global__ __launch_bounds__(kThreads) void sq_fmm_kernel(SqWs w, double bscale, int pub) {
     __shared__ FmmLds L;
     const Img m = image(w, blockIdx.x);
     const uint32_t nb = m.meta[0];
@@ -1084,12 +1145,19 @@ __global__ __launch_bounds__(kThreads) void sq_fmm_kernel(SqWs w, double bscale)
     // meta[25] inner; tools/seq_time.py) -- those words hold the large-bucket
     // probe clocks in OFD_SQ_PROF builds instead
     const uint64_t w0 = threadIdx.x == 0 ? wall_clock64() : 0;
+    if (threadIdx.x == 0 && blockIdx.y == 1) put64(m.pipe + kPTFmm, w0);
     if (blockIdx.y == 0) {
         const Img o = outer_view(m);
         const uint32_t no = fmm_pass<false>(o, m.sO, nb, L, nbk, prof, bscale);
         for (uint32_t i = threadIdx.x; i < no; i += kThreads) {
             const uint32_t p = o.logp[i];
             m.t[p] = -m.t[p];
+        }
+        sync_all();
+        // the ring's distances are final: publish (RECORD reads them)
+        if (threadIdx.x == 0) {
+            put64(m.pipe + kPTOut, wall_clock64());
+            __hip_atomic_store(&m.pipe[kPOutDone], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (threadIdx.x == 0) {
             atomicAdd(&m.meta[4], nbk);
@@ -1099,13 +1167,18 @@ __global__ __launch_bounds__(kThreads) void sq_fmm_kernel(SqWs w, double bscale)
         }
         return;
     }
-    const uint32_t ni = fmm_pass<true>(m, m.sI, nb, L, nbk, prof, bscale);
+    const uint32_t ni = fmm_pass<true>(m, m.sI, nb, L, nbk, prof, bscale, pub != 0);
+    {
+        uint64_t last = 0;
+        publish_prog(m, ni, last, true);  // (fmm_pass ended on a barrier after its last stores)
+    }
     if (threadIdx.x == 0) {
+        put64(m.pipe + kPTIn, wall_clock64());
+        __hip_atomic_store(&m.pipe[kPInDone], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 #ifndef OFD_SQ_PROF
         m.meta[25] = uint32_t(wall_clock64() - w0);
 #endif
         m.meta[1] = ni - nb;
-        m.meta[2] = 0u;
         atomicAdd(&m.meta[4], nbk);
         for (int k = 0; k < 8; ++k) m.meta[8 + k] = uint32_t(k == 6 ? prof[k] : prof[k] >> 8);
 #ifdef OFD_SQ_PROF
@@ -1574,6 +1647,12 @@ constexpr int kRecTH = 16;  // RECORD tile: 64 x kRecTH padded pixels per workgr
 #endif
 
 __global__ __launch_bounds__(256, OFD_REC_MINW) void sq_record3_kernel(SqWs w) {
+    // Only the holes whose stamps lie in this round's window [lo, hi) (the
+    // pacing kernel's snapshot; the whole log in the final round).  Pixels
+    // beyond it may be written by the march while this kernel runs: a racy
+    // stamp read gives INF or a stamp >= hi, both later than any hole
+    // recorded here, and a racy distance is only read where its stamp says
+    // it is not used.
     // The workgroup's 64 x kRecTH pixels with a 4-pixel halo (clamped to the
     // padded image) of stamps and distances in LDS: every window read below
     // is an LDS read.  The tile's holes (~a fifth of its pixels) are listed
@@ -1587,6 +1666,8 @@ __global__ __launch_bounds__(256, OFD_REC_MINW) void sq_record3_kernel(SqWs w) {
     const int i0 = int(blockIdx.y) * kRecTH - 4, j0 = int(blockIdx.x) * 64 - 4;
     const Img m = image(w, blockIdx.z);
     const int eh = m.eh, ew = m.ew;
+    const uint32_t lo = m.pipe[kPLo], hi = m.pipe[kPHi];
+    if (lo >= hi) return;  // uniform: nothing of this image in the window
     if (threadIdx.x == 0) nh = 0u;
     for (int e = threadIdx.x; e < TR * TC; e += 256) {
         const int r = e / TC, c = e - r * TC;
@@ -1599,7 +1680,7 @@ __global__ __launch_bounds__(256, OFD_REC_MINW) void sq_record3_kernel(SqWs w) {
         const int li = 4 + e / 64, lj = 4 + (e & 63);
         const int i = i0 + li, j = j0 + lj;
         const uint32_t sv = Ls[li][lj];
-        const bool hole = i >= 1 && j >= 1 && i < eh - 1 && j < ew - 1 && sv != 0u && sv != INF;
+        const bool hole = i >= 1 && j >= 1 && i < eh - 1 && j < ew - 1 && sv != 0u && sv >= lo && sv < hi;
         const uint64_t bal = __ballot(hole);
         uint32_t base = 0;
         if ((threadIdx.x & 63) == 0 && bal) base = atomicAdd(&nh, uint32_t(__popcll(bal)));
@@ -1619,7 +1700,8 @@ __global__ __launch_bounds__(256, OFD_REC_MINW) void sq_record3_kernel(SqWs w) {
         // COLOUR3 can address a dependant's record without a lookup
         const uint32_t idx = uint32_t(p);
         // Kahn counter and dependants: window positions inside the image (the
-        // tile's clamped halo holds the image's own pixels there)
+        // tile's clamped halo holds the image's own pixels there).  A hole not
+        // pushed yet (INF) is a later one: a dependant.
         uint32_t cnt = 0;
         uint64_t dep = 0;
         int bit = 0;
@@ -1632,7 +1714,7 @@ __global__ __launch_bounds__(256, OFD_REC_MINW) void sq_record3_kernel(SqWs w) {
                 if (y >= 1 && x >= 1 && y < eh - 1 && x < ew - 1) {
                     const uint32_t q = S(y, x);
                     cnt += (q != 0u && q < s) ? 1u : 0u;
-                    if (q > s && q != INF) dep |= uint64_t(1) << bit;
+                    if (q > s) dep |= uint64_t(1) << bit;
                 }
                 ++bit;
             }
@@ -1684,8 +1766,11 @@ __global__ __launch_bounds__(256, OFD_REC_MINW) void sq_record3_kernel(SqWs w) {
         uint4 *dstp = reinterpret_cast<uint4 *>(m.rec + size_t(idx) * kRecW);
 #pragma unroll
         for (int k = 0; k < kRecW / 4; ++k) dstp[k] = make_uint4(r[4 * k], r[4 * k + 1], r[4 * k + 2], r[4 * k + 3]);
-        m.own[p] = (idx << 6) | cnt;  // cnt <= 60; idx = p < en < 2^26 (the launcher's bound)
-        if (cnt == 0u) m.k0[atomicAdd(&m.meta[2], 1u)] = (uint64_t(idx) << 32) | uint64_t(p);
+        // Kahn counter: kK - cnt here, + 1 per release of an earlier hole
+        // (COLOUR3, before or after this): ready at kK, whoever adds last
+        // (cnt <= 60 < kK, so the releases alone never reach it)
+        const uint32_t add = kK - cnt;
+        if (atomicAdd(&m.kc[p], add) + add == kK) m.rq[atomicAdd(&m.meta[2], 1u)] = (uint64_t(idx) << 32) | uint64_t(p);
     }
 }
 
@@ -1721,9 +1806,17 @@ __global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, int C, int H, 
 #define VC(k) (tb[k] & 0xFF)
 #define WC(k) ((tb[k] >> 8) & 0xFF)
 #define DC(k) (tb[k] >> 16)
-    uint64_t *ga = m.k0, *gb = m.fr2;
+    // this round's first level: the ready queue's new entries (RECORD's
+    // holes whose earlier neighbours are all coloured); later levels' entries
+    // past the LDS capacity alternate between fr2 and fr3
+    const uint32_t q0 = m.pipe[kPRqc], q1 = m.meta[2];
+    uint64_t *ga = m.rq + q0, *gb = m.fr2;
     int cur = 0;
-    uint32_t n = m.meta[2], levels = 0, rounds = 0, small = 0;
+    uint32_t n = q1 - q0, levels = 0, rounds = 0, small = 0;
+    if (tid == 0 && n) {
+        if (m.pipe[kPCRounds] == 0u) put64(m.pipe + kPTc0, wall_clock64());
+        m.pipe[kPCRounds] += 1u;
+    }
     for (uint32_t e = tid; e < n && e < uint32_t(kFrCap); e += 1024) L.fr[0][e] = ga[e];
     if (tid == 0) L.nnext[0] = 0u;
     __syncthreads();
@@ -1786,17 +1879,17 @@ __global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, int C, int H, 
                 old[k] = 0;
                 if (act && gl + kL3 * k < kWin && ((dep >> (gl + kL3 * k)) & 1u)) {
                     const int64_t q = int64_t(p) + int64_t(WC(k) / 9 - 4) * ew + (WC(k) % 9 - 4);
-                    old[k] = atomicSub(&m.own[q], 1u);
+                    old[k] = atomicAdd(&m.kc[q], 1u);
                 }
             }
             // the holes whose last earlier neighbour this was join the next level
             auto append_ready = [&]() {
 #pragma unroll
                 for (int k = 0; k < 8; ++k)
-                    if ((old[k] & 63u) == 1u) {
+                    if (old[k] + 1u == kK) {
                         const uint32_t f = atomicAdd(&L.nnext[lv], 1u);
                         const int64_t q = int64_t(p) + int64_t(WC(k) / 9 - 4) * ew + (WC(k) % 9 - 4);
-                        const uint64_t en = (uint64_t(old[k] >> 6) << 32) | uint64_t(q);
+                        const uint64_t en = (uint64_t(q) << 32) | uint64_t(q);
                         if (f < uint32_t(kFrCap))
                             L.fr[cur ^ 1][f] = en;
                         else
@@ -1912,20 +2005,70 @@ __global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, int C, int H, 
         n = L.nnext[lv];
         lv = lv == 2 ? 0 : lv + 1;
         cur ^= 1;
-        uint64_t *tmp = ga;
         ga = gb;
-        gb = tmp;
+        gb = gb == m.fr2 ? m.fr3 : m.fr2;
     }
     if (tid == 0) {
-        m.meta[3] = levels;
-        m.meta[6] = rounds;  // load rounds of kSlots3 holes (levels of more holes take several)
-        m.meta[7] = small;   // levels of at most kSlots3 / 2 holes
+        if (q1 > q0) put64(m.pipe + kPTc1, wall_clock64());
+        m.pipe[kPRqc] = q1;
+        m.meta[3] += levels;
+        m.meta[6] += rounds;  // load rounds of kSlots3 holes (levels of more holes take several)
+        m.meta[7] += small;   // levels of at most kSlots3 / 2 holes
         for (int k = 0; k < 8; ++k) m.meta[16 + k] = uint32_t(prof[k] >> 8);
     }
 }
 #undef VC
 #undef WC
 #undef DC
+
+// Pacing of the pipelined fill's RECORD / COLOUR3 rounds (one workgroup).
+// Round e first waits -- bounded by bound_ticks -- until round_ticks * (e + 1)
+// after round 0 began, or until every image's two marches are done; then it
+// snapshots each image's RECORD window [recdone, hi): hi is the inner march's
+// published progress once its outer march is done (RECORD reads the ring's
+// distances), else nothing.  fin: the marches have completed (stream order),
+// no wait, the window runs to the end of the log.  Never waits on anything
+// without a time bound, so a march that is not resident yet only delays.
+__global__ __launch_bounds__(256) void sq_pace_kernel(SqWs w, int nimg, int e, int fin, uint64_t round_ticks,
+                                                     uint64_t bound_ticks) {
+    uint32_t *t0w = w.pipe + kPT0;  // image 0's pipe words hold the clock origin
+    if (!fin) {
+        if (threadIdx.x == 0) {
+            const uint64_t now = wall_clock64();
+            uint64_t t0 = now;
+            if (e == 0) {
+                t0w[0] = uint32_t(t0);
+                t0w[1] = uint32_t(t0 >> 32);
+            } else {
+                t0 = uint64_t(t0w[0]) | (uint64_t(t0w[1]) << 32);
+            }
+            const uint64_t until = t0 + round_ticks * uint64_t(e + 1);
+            for (;;) {
+                const uint64_t tn = wall_clock64();
+                if (tn >= until || tn - now >= bound_ticks) break;
+                bool done = true;
+                for (int b = 0; b < nimg && done; ++b) {
+                    const uint32_t *pp = w.pipe + int64_t(b) * kPipe;
+                    done = __hip_atomic_load(pp + kPInDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u &&
+                           __hip_atomic_load(pp + kPOutDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+                }
+                if (done) break;
+                __builtin_amdgcn_s_sleep(64);
+            }
+        }
+        __syncthreads();
+    }
+    for (int b = threadIdx.x; b < nimg; b += 256) {
+        uint32_t *pp = w.pipe + int64_t(b) * kPipe;
+        const uint32_t od = __hip_atomic_load(pp + kPOutDone, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t prog = __hip_atomic_load(pp + kPProg, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t lo = pp[kPRecDone];
+        const uint32_t hi = (od != 0u && prog > lo) ? prog : lo;
+        pp[kPLo] = lo;
+        pp[kPHi] = hi;
+        pp[kPRecDone] = hi;
+    }
+}
 
 // The record path's result: every pixel's colours from the shadow image
 // (kept pixels hold PREP's uint8 cast, holes their fill), as float32.
@@ -1989,6 +2132,32 @@ SeqHelpers *seq_helpers(int dev) {
 #ifndef OFD_SEQ_GROUPS_DEFAULT
 #define OFD_SEQ_GROUPS_DEFAULT 1
 #endif
+// Pipelined radius-3 fill (ofd_inpaint_seq_set_pipeline): record / colour
+// rounds on a helper stream beside the marches.  -1 = not set (OFD_SEQ_PIPE
+// rounds, default 12; OFD_SEQ_PIPE_US per round, default 1200).
+int g_pipe_rounds = -1, g_pipe_us = -1;
+int pipe_rounds_setting() {
+    if (g_pipe_rounds < 0) {
+        const char *e = getenv("OFD_SEQ_PIPE");
+        g_pipe_rounds = e ? atoi(e) : 12;
+        if (g_pipe_rounds < 0) g_pipe_rounds = 0;
+        if (g_pipe_rounds > 256) g_pipe_rounds = 256;
+    }
+    return g_pipe_rounds;
+}
+int pipe_us_setting() {
+    if (g_pipe_us < 0) {
+        const char *e = getenv("OFD_SEQ_PIPE_US");
+        g_pipe_us = e ? atoi(e) : 1200;
+        if (g_pipe_us < 1) g_pipe_us = 1;
+    }
+    return g_pipe_us;
+}
+// images below this many pixels: marches too short to overlap (unless a
+// test forces the pipeline with ofd_inpaint_seq_set_pipeline(rounds, us, 1))
+int g_pipe_force = 0;
+constexpr int64_t kPipeMinPixels = int64_t(1) << 18;
+
 int g_seq_groups = -1;  // ofd_inpaint_seq_set_groups; -1 = not set (OFD_SEQ_GROUPS, else the default)
 int seq_groups_setting() {
     if (g_seq_groups < 0) {
@@ -2027,6 +2196,15 @@ int ofd_inpaint_seq_helper_device(void *stream) {
     const int dev = stream_device(static_cast<hipStream_t>(stream));
     SeqHelpers *h = seq_helpers(dev);
     return h && h->ok ? h->device : -1;
+}
+
+int ofd_inpaint_seq_set_pipeline(int rounds, int round_us, int force) {
+    const int prev = pipe_rounds_setting();
+    (void)pipe_us_setting();
+    if (rounds >= 0) g_pipe_rounds = rounds > 256 ? 256 : rounds;
+    if (round_us >= 1) g_pipe_us = round_us;
+    if (force >= 0) g_pipe_force = force ? 1 : 0;
+    return prev;
 }
 
 int ofd_inpaint_seq_set_groups(int groups) {
@@ -2072,6 +2250,15 @@ int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float 
         return e ? atof(e) : 0.7;
     }();
     const double bscale = (H + W < 8000 && wide > 0.0 && wide <= 0.7) ? 1.0 / wide : 2.0;
+    // pipelined rounds (radius-3 path only; one group: the helper stream is the pipeline's)
+    int rounds = (H * W >= kPipeMinPixels || g_pipe_force) ? pipe_rounds_setting() : 0;
+    uint64_t pipe_ticks = 0;
+    if (rounds > 0) {
+        int dev = stream_device(st), khz = 0;
+        if (dev < 0 || hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0)
+            khz = 100000;  // the MI355X's 100 MHz constant clock
+        pipe_ticks = uint64_t(pipe_us_setting()) * uint64_t(khz) / 1000u;
+    }
     // one chunk of nb images (workspace w) on stream s
     auto run_chunk = [&](const SqWs &w, int64_t b0, int64_t nb, hipStream_t s) {
         hipLaunchKernelGGL(sq_prep_tile_kernel, dim3(unsigned((W + 63) / 64), unsigned((H + 15) / 16), unsigned(nb)),
@@ -2085,15 +2272,39 @@ int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float 
             hipLaunchKernelGGL(sq_init_kernel, dim3(unsigned((w.eh + 3) / 4), unsigned(nb)), dim3(256), 0, s, w, r);
         hipLaunchKernelGGL(sq_band_scan_kernel, dim3(unsigned(nb)), dim3(kThreads), 0, s, w);
         hipLaunchKernelGGL(sq_band_write_kernel, dim3(unsigned((w.eh + 3) / 4), unsigned(nb)), dim3(256), 0, s, w);
-        hipLaunchKernelGGL(sq_fmm_kernel, dim3(unsigned(nb), 2u), dim3(kThreads), 0, s, w, bscale);
+        const dim3 rgrid(unsigned((w.ew + 63) / 64), unsigned((w.eh + kRecTH - 1) / kRecTH), unsigned(nb));
+        auto round = [&](hipStream_t rs, int e, int fin) {  // one RECORD / COLOUR3 round
+            hipLaunchKernelGGL(sq_pace_kernel, dim3(1), dim3(256), 0, rs, w, int(nb), e, fin, pipe_ticks, 4 * pipe_ticks);
+            hipLaunchKernelGGL(sq_record3_kernel, rgrid, dim3(256), 0, rs, w);
+            hipLaunchKernelGGL(sq_colour3_kernel, dim3(unsigned(nb)), dim3(1024), 0, rs, w, int(C), int(H), int(W));
+        };
+        // Pipelined (radius 3, C <= 3, large images): while the marches run
+        // on s, a helper stream runs `rounds` RECORD / COLOUR3 rounds over the
+        // holes the inner march has finished, so the colour chain overlaps
+        // the march instead of following it; the final round on s (after the
+        // marches) takes whatever is left.  Every round's result is the same:
+        // counters are additive and the colour order is the Kahn order.
+        SeqHelpers *hp = nullptr;
+        if (rec3 && rounds > 0) {
+            hp = seq_helpers(stream_device(s));
+            if (hp && !hp->ok) hp = nullptr;
+        }
+        if (hp) {
+            std::lock_guard<std::mutex> lk(hp->mu);
+            (void)hipEventRecord(hp->fork, s);  // after BAND: the helper may start reading
+            (void)hipStreamWaitEvent(hp->stream[0], hp->fork, 0);
+            hipLaunchKernelGGL(sq_fmm_kernel, dim3(unsigned(nb), 2u), dim3(kThreads), 0, s, w, bscale, 1);
+            for (int e = 0; e < rounds; ++e) round(hp->stream[0], e, 0);
+            (void)hipEventRecord(hp->join[0], hp->stream[0]);
+            (void)hipStreamWaitEvent(s, hp->join[0], 0);
+        } else {
+            hipLaunchKernelGGL(sq_fmm_kernel, dim3(unsigned(nb), 2u), dim3(kThreads), 0, s, w, bscale, 0);
+        }
 #ifdef OFD_BUCKET_TRACE
         return;  // probe: keep the record area (the inner march's bucket trace) for the host
 #endif
         if (rec3) {
-            hipLaunchKernelGGL(sq_record3_kernel,
-                               dim3(unsigned((w.ew + 63) / 64), unsigned((w.eh + kRecTH - 1) / kRecTH), unsigned(nb)),
-                               dim3(256), 0, s, w);
-            hipLaunchKernelGGL(sq_colour3_kernel, dim3(unsigned(nb)), dim3(1024), 0, s, w, int(C), int(H), int(W));
+            round(s, 0, 1);
             hipLaunchKernelGGL(sq_unpack_kernel, dim3(unsigned((H * W + 255) / 256), unsigned(nb)), dim3(256), 0, s, w,
                                out, int(C), int64_t(H * W), b0);
             return;
@@ -2117,6 +2328,7 @@ int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float 
         const SqWs w = carve(workspace, G, H, W);
         for (int64_t b0 = 0; b0 < B; b0 += G) run_chunk(w, b0, B - b0 < G ? B - b0 : G, st);
     } else {
+        rounds = 0;  // the helper streams carry the groups (and their mutex is held below)
         SeqHelpers *hpp = seq_helpers(stream_device(st));
         if (!hpp || !hpp->ok) return OFD_FW_EWORKSPACE;
         SeqHelpers &hp = *hpp;

@@ -542,3 +542,55 @@ def test_inpaint_sequential_helpers_follow_the_stream_device(cuda_device):
             assert lib.ofd_inpaint_seq_helper_device(ctypes.c_void_p(s.cuda_stream)) == d
         with torch.cuda.device(d):
             assert lib.ofd_inpaint_seq_helper_device(None) == d  # the null stream: the current device
+
+
+# ------------------------------------------------------------------ pipelined record / colour rounds
+@pytest.fixture
+def seq_pipeline():
+    """Sets the pipelined fill's rounds for one test (ofd_inpaint_seq_set_pipeline)
+    and restores the defaults afterwards."""
+    from opticalflowfromdepth_amd import _native
+    lib = _native.lib()
+    prev = lib.ofd_inpaint_seq_set_pipeline(-1, -1, -1)
+
+    def set_(rounds, us, force):
+        lib.ofd_inpaint_seq_set_pipeline(rounds, us, force)
+    yield set_
+    lib.ofd_inpaint_seq_set_pipeline(prev, 1200, 0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", _gpu_cases() + _seq_extra_cases(), ids=lambda c: c[0])
+def test_inpaint_sequential_pipelined_rounds_bit_exact(case, seq_pipeline):
+    """The RECORD / COLOUR3 rounds running beside the marches (forced on these
+    small images, 64 rounds 2 us apart, so rounds interleave with every stage
+    of the march): cv2's order bit for bit, as the unpipelined fill."""
+    from opticalflowfromdepth_amd import ops
+    name, img, v, c, r = case
+    dev = torch.device("cuda:0")
+    seq_pipeline(64, 2, 1)
+    got = ops.inpaint(torch.from_numpy(img).to(dev), torch.from_numpy(v).to(dev), torch.from_numpy(c).to(dev),
+                      radius=r, order="sequential").cpu().numpy()
+    exp = oracle.inpaint(img, v, c, r, layered=False)
+    bad = np.argwhere(got != exp)
+    assert bad.size == 0, f"{name}: {len(bad)} differing values, first {bad[:5].tolist()}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rounds,us", [(0, 1200), (12, 1200), (48, 100), (4, 5000)])
+def test_inpaint_sequential_pipeline_settings_agree_on_warped_images(rounds, us, seq_pipeline):
+    """Warped 768x1024 images (disparity and ego-motion holes, 8 at once), with
+    no rounds, the default rounds, many short rounds and a few long ones: the
+    same bits, equal to the oracle's cv2 order."""
+    from opticalflowfromdepth_amd import forward_warp_flow, ops, synth
+    dev = torch.device("cuda:0")
+    seeds = [12345, 12346, 12377, 12378, 12401, 12402, 12433, 12434]
+    obj, flow, depth = synth.stage_one_batch(seeds, 768, 1024, dev)
+    out, valid, coll = forward_warp_flow(obj, flow, depth)
+    rgb = (out[:, 0:3] * valid).contiguous()
+    seq_pipeline(rounds, us, 0)
+    got = ops.inpaint(rgb, valid, coll, order="sequential").cpu().numpy()
+    exp = oracle.inpaint(rgb.cpu().numpy(), valid.cpu().numpy(), coll.cpu().numpy(), 3, layered=False)
+    assert np.array_equal(got, exp)
+    from opticalflowfromdepth_amd import _native
+    assert _native.lib().ofd_inpaint_faults(1) == 0

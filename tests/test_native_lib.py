@@ -103,6 +103,12 @@ def test_schedule_setters_are_host_state():
     assert lib.ofd_fw_set_pack(1 - pk) == pk
     assert lib.ofd_fw_set_pack(7) == 1 - pk  # only queries
     lib.ofd_fw_set_pack(pk)
+    pr = lib.ofd_inpaint_seq_set_pipeline(-1, -1, -1)
+    assert pr >= 0
+    assert lib.ofd_inpaint_seq_set_pipeline(5, 300, 0) == pr
+    assert lib.ofd_inpaint_seq_set_pipeline(999, -1, -1) == 5  # clamps to 256
+    assert lib.ofd_inpaint_seq_set_pipeline(-1, -1, -1) == 256
+    lib.ofd_inpaint_seq_set_pipeline(pr, 1200, 0)
     g = lib.ofd_inpaint_seq_set_groups(-1)
     assert 1 <= g <= 4
     assert lib.ofd_inpaint_seq_set_groups(9) == g

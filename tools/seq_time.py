@@ -18,10 +18,23 @@ def a256(x):
 def seq_meta(ws, B, H, W):
     eh, ew = H + 2, W + 2
     en = eh * ew
-    pi = a256(en * 4) * 6 + a256(en * 8) * 2 + a256(eh * 4) + 32 * 4 + en * 160 + H * W * 4 + en * 8 + 768
+    pi = (a256(en * 4) * 6 + a256(en * 8) * 2 + a256(eh * 4) + 32 * 4 + en * 160 + H * W * 4 + en * 8 + 768
+          + en * 8 + en * 24 + en * 8 + en * 4 + en * 8 + 64 * 4 + 6 * 256)
     G = min(B, (ws.numel() - 2048) // pi)
     off = 6 * a256(G * en * 4) + 2 * a256(G * en * 8) + a256(G * eh * 4)
     return ws[off:off + G * 32 * 4].view(torch.int32).view(G, 32).cpu().numpy()
+
+
+def seq_pipe(ws, B, H, W):
+    """The pipelined fill's per-image control / timeline words (kPipe = 64 per
+    image, after the ready queue; csrc/ofd_inpaint_seq.hip carve())."""
+    eh, ew = H + 2, W + 2
+    en, hw = eh * ew, H * W
+    G = B
+    off = (6 * a256(G * en * 4) + 2 * a256(G * en * 8) + a256(G * eh * 4) + a256(G * 32 * 4) + a256(G * en * 160)
+           + a256(G * hw * 4) + 2 * a256(G * en * 8) + a256(G * en * 24) + a256(G * en * 8) + a256(G * en * 4)
+           + a256(G * en * 8))
+    return ws[off:off + G * 64 * 4].view(torch.int32).view(G, 64).cpu().numpy().astype(np.int64) & 0xFFFFFFFF
 
 
 def main():
@@ -55,6 +68,17 @@ def main():
             print(f"  image {int(k)}: outer {o[k]:.0f} us, inner {i[k]:.0f} us, levels {int(m[k, 3])}")
     for k in np.argsort(-m[:, 3])[:8]:
         print(k, m[k, :8].tolist())
+    pp = seq_pipe(ws, B, 768, 1024)
+    t = lambda c: (pp[:, c] | (pp[:, c + 1] << 32)).astype(np.float64)  # noqa: E731
+    t0 = t(8).min()
+    if t0 > 0:  # pipelined-fill timeline of the last call (us from the first march's start)
+        rel = lambda c: np.where(t(c) > 0, (t(c) - t0) / 100.0, np.nan)  # noqa: E731
+        fo, fi, c0, c1 = rel(10), rel(12), rel(40), rel(42)
+        print(f"timeline (us): outer end max {np.nanmax(fo):.0f}, inner end max {np.nanmax(fi):.0f}, "
+              f"colour end max {np.nanmax(c1):.0f} (image {int(np.nanargmax(c1))})")
+        for k in np.argsort(-np.nan_to_num(c1))[:6]:
+            print(f"  image {int(k)}: outer end {fo[k]:.0f}, inner end {fi[k]:.0f}, colour {c0[k]:.0f} .. {c1[k]:.0f}"
+                  f" in {int(pp[k, 44])} rounds, levels {int(m[k, 3])}")
     eh, ew = 770, 1026
     en = eh * ew
     pi_ = a256(en * 4) * 6 + a256(en * 8) * 2 + a256(eh * 4) + 32 * 4 + en * 160 + 768 * 1024 * 4 + en * 8 + 768
