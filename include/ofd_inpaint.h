@@ -110,7 +110,7 @@ int ofd_inpaint_seq_set_groups(int groups);
  * takes the rest.  rounds = 0 runs the record and colour passes after the
  * marches only.  force = 1 pipelines smaller images too (tests).  Results
  * never depend on any of it.  Negative values leave a setting as it is;
- * defaults OFD_SEQ_PIPE (12) and OFD_SEQ_PIPE_US (1200).  Process-wide;
+ * defaults OFD_SEQ_PIPE (0: off) and OFD_SEQ_PIPE_US (1200).  Process-wide;
  * returns the previous number of rounds.  Grouped fills
  * (ofd_inpaint_seq_set_groups > 1) are not pipelined. */
 int ofd_inpaint_seq_set_pipeline(int rounds, int round_us, int force);

@@ -2134,12 +2134,12 @@ SeqHelpers *seq_helpers(int dev) {
 #endif
 // Pipelined radius-3 fill (ofd_inpaint_seq_set_pipeline): record / colour
 // rounds on a helper stream beside the marches.  -1 = not set (OFD_SEQ_PIPE
-// rounds, default 12; OFD_SEQ_PIPE_US per round, default 1200).
+// rounds, default 0 = off; OFD_SEQ_PIPE_US per round, default 1200).
 int g_pipe_rounds = -1, g_pipe_us = -1;
 int pipe_rounds_setting() {
     if (g_pipe_rounds < 0) {
         const char *e = getenv("OFD_SEQ_PIPE");
-        g_pipe_rounds = e ? atoi(e) : 12;
+        g_pipe_rounds = e ? atoi(e) : 0;
         if (g_pipe_rounds < 0) g_pipe_rounds = 0;
         if (g_pipe_rounds > 256) g_pipe_rounds = 256;
     }
