@@ -1768,9 +1768,13 @@ __global__ __launch_bounds__(256, OFD_REC_MINW) void sq_record3_kernel(SqWs w) {
         for (int k = 0; k < kRecW / 4; ++k) dstp[k] = make_uint4(r[4 * k], r[4 * k + 1], r[4 * k + 2], r[4 * k + 3]);
         // Kahn counter: kK - cnt here, + 1 per release of an earlier hole
         // (COLOUR3, before or after this): ready at kK, whoever adds last
-        // (cnt <= 60 < kK, so the releases alone never reach it)
-        const uint32_t add = kK - cnt;
-        if (atomicAdd(&m.kc[p], add) + add == kK) m.rq[atomicAdd(&m.meta[2], 1u)] = (uint64_t(idx) << 32) | uint64_t(p);
+        // (cnt <= 60 < kK, so the releases alone never reach it).  No COLOUR3
+        // runs while RECORD does (one stream orders the rounds), so the
+        // releases so far are a plain read and the sum a plain store (a
+        // returning atomic per hole cost ~10 ms per 64 images).
+        const uint32_t rel = m.kc[p];
+        m.kc[p] = kK - cnt + rel;
+        if (rel == cnt) m.rq[atomicAdd(&m.meta[2], 1u)] = (uint64_t(idx) << 32) | uint64_t(p);
     }
 }
 
@@ -1779,6 +1783,9 @@ struct C3Lds {
     uint64_t fr[2][kFrCap];
     float buf[kSlots3][kBufStride];  // per hole: the 9x9 colour grid (81 words), then the terms
     float res[kSlots3][9];       // per hole: chain results (Ia, Jx, Jy per channel)
+#if OFD_C3_PF
+    uint32_t dump[64];  // prefetch loads' discarded words
+#endif
 };
 
 __global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, int C, int H, int W) {
@@ -1879,11 +1886,25 @@ __global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, int C, int H, 
                 old[k] = 0;
                 if (act && gl + kL3 * k < kWin && ((dep >> (gl + kL3 * k)) & 1u)) {
                     const int64_t q = int64_t(p) + int64_t(WC(k) / 9 - 4) * ew + (WC(k) % 9 - 4);
+#if OFD_C3_PF
+                    // the dependant's record (two 128-byte lines) towards this
+                    // CU: a later level loads it (into a discarded LDS word)
+                    const uint32_t *qr = m.rec + size_t(q) * kRecW;
+                    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)qr,
+                                                     (__attribute__((address_space(3))) void *)L.dump, 4, 0, 0);
+                    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(qr + kRecW - 1),
+                                                     (__attribute__((address_space(3))) void *)L.dump, 4, 0, 0);
+#endif
                     old[k] = atomicAdd(&m.kc[q], 1u);
                 }
             }
             // the holes whose last earlier neighbour this was join the next level
             auto append_ready = [&]() {
+                // the returned counters stay opaque until here: otherwise the
+                // compiler folds each into its compare at once and waits for
+                // every atomic in turn (eight round trips per level, ~+35% time)
+                asm volatile("" : "+v"(old[0]), "+v"(old[1]), "+v"(old[2]), "+v"(old[3]), "+v"(old[4]), "+v"(old[5]),
+                             "+v"(old[6]), "+v"(old[7]));
 #pragma unroll
                 for (int k = 0; k < 8; ++k)
                     if (old[k] + 1u == kK) {
