@@ -105,13 +105,15 @@ int ofd_inpaint_seq_set_groups(int groups);
 
 /* The pipelined sequential fill (radius 3, C <= 3 -- utils.inpaint's call --
  * on images of at least 2^18 pixels): `rounds` record / colour rounds run on
- * a helper stream beside the fast marches, each about `round_us` apart, over
- * the holes the inner march has finished; the final round after the marches
- * takes the rest.  rounds = 0 runs the record and colour passes after the
- * marches only.  force = 1 pipelines smaller images too (tests).  Results
- * never depend on any of it.  Negative values leave a setting as it is;
- * defaults OFD_SEQ_PIPE (0: off) and OFD_SEQ_PIPE_US (1200).  Process-wide;
- * returns the previous number of rounds.  Grouped fills
+ * a helper stream beside the fast marches, `round_us` apart, over the holes
+ * the inner march has finished (once the image's outer march is done); each
+ * colour round stops at the next round's start and carries its frontier
+ * over, and the final round after the marches takes the rest.  rounds = 0
+ * runs the record and colour passes after the marches only.  force = 1
+ * pipelines smaller images too (tests).  Results never depend on any of it.
+ * Negative values leave a setting as it is, round_us = 0 restores its
+ * default; defaults OFD_SEQ_PIPE (else 12) and OFD_SEQ_PIPE_US (else 2000).
+ * Process-wide; returns the previous number of rounds.  Grouped fills
  * (ofd_inpaint_seq_set_groups > 1) are not pipelined. */
 int ofd_inpaint_seq_set_pipeline(int rounds, int round_us, int force);
 

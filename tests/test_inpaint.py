@@ -556,7 +556,7 @@ def seq_pipeline():
     def set_(rounds, us, force):
         lib.ofd_inpaint_seq_set_pipeline(rounds, us, force)
     yield set_
-    lib.ofd_inpaint_seq_set_pipeline(prev, 1200, 0)
+    lib.ofd_inpaint_seq_set_pipeline(prev, 0, 0)
 
 
 @pytest.mark.gpu
@@ -577,7 +577,7 @@ def test_inpaint_sequential_pipelined_rounds_bit_exact(case, seq_pipeline):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("rounds,us", [(0, 1200), (12, 1200), (48, 100), (4, 5000)])
+@pytest.mark.parametrize("rounds,us", [(0, 2000), (12, 2000), (48, 100), (4, 5000)])
 def test_inpaint_sequential_pipeline_settings_agree_on_warped_images(rounds, us, seq_pipeline):
     """Warped 768x1024 images (disparity and ego-motion holes, 8 at once), with
     no rounds, the default rounds, many short rounds and a few long ones: the

@@ -108,7 +108,7 @@ def test_schedule_setters_are_host_state():
     assert lib.ofd_inpaint_seq_set_pipeline(5, 300, 0) == pr
     assert lib.ofd_inpaint_seq_set_pipeline(999, -1, -1) == 5  # clamps to 256
     assert lib.ofd_inpaint_seq_set_pipeline(-1, -1, -1) == 256
-    lib.ofd_inpaint_seq_set_pipeline(pr, 1200, 0)
+    lib.ofd_inpaint_seq_set_pipeline(pr, 0, 0)
     g = lib.ofd_inpaint_seq_set_groups(-1)
     assert 1 <= g <= 4
     assert lib.ofd_inpaint_seq_set_groups(9) == g

@@ -27,13 +27,13 @@ def seq_meta(ws, B, H, W):
 
 def seq_pipe(ws, B, H, W):
     """The pipelined fill's per-image control / timeline words (kPipe = 64 per
-    image, after the ready queue; csrc/ofd_inpaint_seq.hip carve())."""
+    image, after the ready queue and the carry buffer; csrc/ofd_inpaint_seq.hip carve())."""
     eh, ew = H + 2, W + 2
     en, hw = eh * ew, H * W
     G = B
     off = (6 * a256(G * en * 4) + 2 * a256(G * en * 8) + a256(G * eh * 4) + a256(G * 32 * 4) + a256(G * en * 160)
            + a256(G * hw * 4) + 2 * a256(G * en * 8) + a256(G * en * 24) + a256(G * en * 8) + a256(G * en * 4)
-           + a256(G * en * 8))
+           + a256(G * en * 8) + a256(G * en * 8))
     return ws[off:off + G * 64 * 4].view(torch.int32).view(G, 64).cpu().numpy().astype(np.int64) & 0xFFFFFFFF
 
 
