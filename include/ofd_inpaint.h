@@ -117,6 +117,16 @@ int ofd_inpaint_seq_set_groups(int groups);
  * (ofd_inpaint_seq_set_groups > 1) are not pipelined. */
 int ofd_inpaint_seq_set_pipeline(int rounds, int round_us, int force);
 
+/* Chip-wide early buckets of the sequential fill's two fast marches: up to
+ * `buckets` buckets of each march run as launches over every march of the
+ * chunk at once (the band- and ring-sized first buckets), until a march has
+ * fewer than `min_pending` pending log entries; the march's own workgroup
+ * takes over from there.  buckets = 0: off.  Results never depend on it.
+ * Negative values leave a setting as it is; defaults OFD_SEQ_CW (else 0:
+ * off, measured slower than the per-march workgroups) and 16384.
+ * Process-wide; returns the previous number of buckets. */
+int ofd_inpaint_seq_set_chipwide(int buckets, int min_pending);
+
 /* The device whose helper streams a grouped sequential fill on `stream`
  * would use: the stream's own device (helpers are kept per device and
  * created there on first use), or -1 if it cannot be told. */

@@ -576,6 +576,59 @@ def test_inpaint_sequential_pipelined_rounds_bit_exact(case, seq_pipeline):
     assert bad.size == 0, f"{name}: {len(bad)} differing values, first {bad[:5].tolist()}"
 
 
+@pytest.fixture
+def seq_chipwide():
+    """Sets the chip-wide early buckets for one test (ofd_inpaint_seq_set_chipwide)
+    and restores the defaults afterwards."""
+    from opticalflowfromdepth_amd import _native
+    lib = _native.lib()
+    prev = lib.ofd_inpaint_seq_set_chipwide(-1, -1)
+
+    def set_(buckets, min_pending):
+        lib.ofd_inpaint_seq_set_chipwide(buckets, min_pending)
+    yield set_
+    lib.ofd_inpaint_seq_set_chipwide(prev, 16384)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("buckets", [8, 3, 64])
+@pytest.mark.parametrize("case", _gpu_cases() + _seq_extra_cases(), ids=lambda c: c[0])
+def test_inpaint_sequential_chipwide_buckets_bit_exact(case, buckets, seq_chipwide):
+    """The marches' first buckets as chip-wide launches (opt-in; kept chip-wide
+    down to no pending entries: 3 or 8 buckets then the workgroup, or all of
+    them): cv2's order bit for bit."""
+    from opticalflowfromdepth_amd import ops
+    name, img, v, c, r = case
+    dev = torch.device("cuda:0")
+    seq_chipwide(buckets, 0)
+    got = ops.inpaint(torch.from_numpy(img).to(dev), torch.from_numpy(v).to(dev), torch.from_numpy(c).to(dev),
+                      radius=r, order="sequential").cpu().numpy()
+    exp = oracle.inpaint(img, v, c, r, layered=False)
+    bad = np.argwhere(got != exp)
+    assert bad.size == 0, f"{name}: {len(bad)} differing values, first {bad[:5].tolist()}"
+    from opticalflowfromdepth_amd import _native
+    assert _native.lib().ofd_inpaint_faults(1) == 0
+
+
+@pytest.mark.gpu
+def test_inpaint_sequential_chipwide_buckets_on_warped_images(seq_chipwide):
+    """Warped 768x1024 images (8 at once): band- and ring-sized buckets of
+    ~100 k pops, so the chip-wide path's merge passes and multi-chunk scans
+    run; the same bits as the oracle's cv2 order."""
+    from opticalflowfromdepth_amd import forward_warp_flow, ops, synth
+    dev = torch.device("cuda:0")
+    seeds = [12345, 12346, 12377, 12378, 12401, 12402, 12433, 12434]
+    obj, flow, depth = synth.stage_one_batch(seeds, 768, 1024, dev)
+    out, valid, coll = forward_warp_flow(obj, flow, depth)
+    rgb = (out[:, 0:3] * valid).contiguous()
+    seq_chipwide(8, 16384)
+    got = ops.inpaint(rgb, valid, coll, order="sequential").cpu().numpy()
+    exp = oracle.inpaint(rgb.cpu().numpy(), valid.cpu().numpy(), coll.cpu().numpy(), 3, layered=False)
+    assert np.array_equal(got, exp)
+    from opticalflowfromdepth_amd import _native
+    assert _native.lib().ofd_inpaint_faults(1) == 0
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("rounds,us", [(0, 2000), (12, 2000), (48, 100), (4, 5000)])
 def test_inpaint_sequential_pipeline_settings_agree_on_warped_images(rounds, us, seq_pipeline):

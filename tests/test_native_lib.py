@@ -109,6 +109,12 @@ def test_schedule_setters_are_host_state():
     assert lib.ofd_inpaint_seq_set_pipeline(999, -1, -1) == 5  # clamps to 256
     assert lib.ofd_inpaint_seq_set_pipeline(-1, -1, -1) == 256
     lib.ofd_inpaint_seq_set_pipeline(pr, 0, 0)
+    cw = lib.ofd_inpaint_seq_set_chipwide(-1, -1)
+    assert 0 <= cw <= 64
+    assert lib.ofd_inpaint_seq_set_chipwide(3, 0) == cw
+    assert lib.ofd_inpaint_seq_set_chipwide(999, -1) == 3  # clamps to 64
+    assert lib.ofd_inpaint_seq_set_chipwide(-1, -1) == 64
+    lib.ofd_inpaint_seq_set_chipwide(cw, 16384)
     g = lib.ofd_inpaint_seq_set_groups(-1)
     assert 1 <= g <= 4
     assert lib.ofd_inpaint_seq_set_groups(9) == g
