@@ -649,7 +649,7 @@ def main(argv=None):
     cfg2 = None
     if rank == 0 and not args.no_config2:
         progress("config 2")
-        cfg2 = config2_phase(20, dev, stream, threads, args.cpu_seconds / 2 if cpu_on else 0)
+        cfg2 = config2_phase(60, dev, stream, threads, args.cpu_seconds / 2 if cpu_on else 0)
 
     fused = fused_ego = None
     if rank == 0 and not args.no_fused:
