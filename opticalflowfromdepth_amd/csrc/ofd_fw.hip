@@ -71,6 +71,10 @@ constexpr unsigned int IDX_NONE = ~0u;
 #define OFD_PROBE_TH 32
 #endif
 constexpr int TW = OFD_PROBE_TW, TH = OFD_PROBE_TH;  // target tile (LDS z-buffer 32 KiB)
+// Only the 128 x 32 tile is supported since the packed targets (round 5): a
+// 128 x 16 probe build faulted on the GPU (illegal address), so other shapes
+// no longer compile.
+static_assert(TW == 128 && TH == 32, "tile engine: 128 x 32 tiles only");
 constexpr int SBW = 16, SBH = 4;          // source block = one wave (64 px)
 constexpr int SEGB = 8;                   // source blocks per segment (128 x 4 px)
 constexpr int MAX_TILES_PER_BLOCK = 12;   // wider boxes go through the global path
