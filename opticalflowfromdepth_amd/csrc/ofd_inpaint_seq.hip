@@ -1840,6 +1840,14 @@ constexpr bool win3(int a, int b) {
     const int a1 = (a < 0 ? -a : a) - 1, b1 = (b < 0 ? -b : b) - 1;
     return (a1 < 0 ? 0 : a1) * (a1 < 0 ? 0 : a1) + (b1 < 0 ? 0 : b1) * (b1 < 0 ? 0 : b1) <= 9;
 }
+// The window positions a hole's colour actually reads when none of its disk
+// pixels is on a border row / column (where cv2's gradient shifts by one):
+// the disk and its 4-neighbours (cv2's gradients are central, forward or
+// backward differences along x and y) -- 48 of win3's 60 neighbours; the 12
+// others, (+-3, +-3), (+-4, +-1), (+-1, +-4), are read only near a border.
+constexpr bool need3(int a, int b) {
+    return disk3(a, b) || disk3(a + 1, b) || disk3(a - 1, b) || disk3(a, b + 1) || disk3(a, b - 1);
+}
 
 // pending[p] = holes of smaller stamp in p's window; level 0 = none
 __global__ __launch_bounds__(256) void sq_count_kernel(SqWs w, int range) {
@@ -2338,7 +2346,14 @@ __global__ __launch_bounds__(256, OFD_REC_MINW) void sq_record3_kernel(SqWs w) {
         const uint32_t idx = uint32_t(p);
         // Kahn counter and dependants: window positions inside the image (the
         // tile's clamped halo holds the image's own pixels there).  A hole not
-        // pushed yet (INF) is a later one: a dependant.
+        // pushed yet (INF) is a later one: a dependant.  h depends on an
+        // earlier q at offset o iff o is among the positions h's colour reads
+        // (need3, or all of win3 for a hole within 4 of the padded border,
+        // whose disk may reach a border row or column); the same predicate,
+        // with q's position, decides whether a later q depends on h (the
+        // position sets are symmetric) -- the counter and the releases agree.
+        const auto near_border = [&](int y, int x) { return y <= 4 || x <= 4 || y >= eh - 5 || x >= ew - 5; };
+        const bool hb = near_border(i, j);
         uint32_t cnt = 0;
         uint64_t dep = 0;
         int bit = 0;
@@ -2350,8 +2365,8 @@ __global__ __launch_bounds__(256, OFD_REC_MINW) void sq_record3_kernel(SqWs w) {
                 const int y = i + a, x = j + b;
                 if (y >= 1 && x >= 1 && y < eh - 1 && x < ew - 1) {
                     const uint32_t q = S(y, x);
-                    cnt += (q != 0u && q < s) ? 1u : 0u;
-                    if (q > s) dep |= uint64_t(1) << bit;
+                    cnt += (q != 0u && q < s && (need3(a, b) || hb)) ? 1u : 0u;
+                    if (q > s && (need3(a, b) || near_border(y, x))) dep |= uint64_t(1) << bit;
                 }
                 ++bit;
             }
