@@ -349,7 +349,9 @@ __global__ __launch_bounds__(256) void sq_prep_tile_kernel(const float *__restri
             else
                 ob[c * HW + p] = float(u);
         }
-        if (shadow) w.shd[bl * w.hw + p] = pk;
+        // (byte 3: the coloured flag of the levels-free colour pass -- set on
+        // kept pixels, by the colour store on holes; no other reader)
+        if (shadow) w.shd[bl * w.hw + p] = pk | (hp == 1u ? 0xFF000000u : 0u);
     }
 }
 
@@ -2355,7 +2357,7 @@ __global__ __launch_bounds__(256, OFD_REC_MINW) void sq_record3_kernel(SqWs w) {
         const auto near_border = [&](int y, int x) { return y <= 4 || x <= 4 || y >= eh - 5 || x >= ew - 5; };
         const bool hb = near_border(i, j);
         uint32_t cnt = 0;
-        uint64_t dep = 0;
+        uint64_t dep = 0, emask = 0;  // emask: the earlier holes counted (the levels-free colour pass waits on them)
         int bit = 0;
 #pragma unroll
         for (int a = -4; a <= 4; ++a)
@@ -2365,7 +2367,10 @@ __global__ __launch_bounds__(256, OFD_REC_MINW) void sq_record3_kernel(SqWs w) {
                 const int y = i + a, x = j + b;
                 if (y >= 1 && x >= 1 && y < eh - 1 && x < ew - 1) {
                     const uint32_t q = S(y, x);
-                    cnt += (q != 0u && q < s && (need3(a, b) || hb)) ? 1u : 0u;
+                    if (q != 0u && q < s && (need3(a, b) || hb)) {
+                        ++cnt;
+                        emask |= uint64_t(1) << bit;
+                    }
                     if (q > s && (need3(a, b) || near_border(y, x))) dep |= uint64_t(1) << bit;
                 }
                 ++bit;
@@ -2414,6 +2419,8 @@ __global__ __launch_bounds__(256, OFD_REC_MINW) void sq_record3_kernel(SqWs w) {
             }
         r[36] = uint32_t(dep);
         r[37] = uint32_t(dep >> 32);
+        r[23] = uint32_t(emask);  // spare weight slots (disk positions 29 and 30 of lanes 5 and 6)
+        r[27] = uint32_t(emask >> 32);
         r[38] = __float_as_uint(sum);
         uint4 *dstp = reinterpret_cast<uint4 *>(m.rec + size_t(idx) * kRecW);
 #pragma unroll
@@ -2723,6 +2730,440 @@ __global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, int C, int H, 
 #undef WC
 #undef DC
 
+
+// COLOUR3 without levels (OFD_SEQ_DF=1, opt-in): the ready holes sit in a
+// queue (fr2, positions carried across rounds in kPQh / kPQt); each wave
+// takes up to 8 of them, colours them with COLOUR3's per-hole code, and
+// queues the holes its releases completed -- no workgroup barrier, so a
+// hole starts as soon as its last earlier neighbour has released it.  The
+// releases are issued before a hole's colour exists (their round trip
+// overlaps the arithmetic), so a hole first waits for each earlier
+// neighbour it reads to carry the coloured flag (byte 3 of its word: PREP
+// sets it on kept pixels, the colour store on holes).  A wave leaves when
+// the queue is empty and no wave holds a hole, or at the deadline (the
+// queue is carried to the next round).  Every wait is bounded (fault 32).
+constexpr int kDfCt = 2048;  // recent-colour table entries
+constexpr int kDfQ = 512;    // queue entries held in LDS (the rest in fr2)
+struct C3DfLds {
+    float buf[kSlots3][kBufStride];
+    float res[kSlots3][9];
+    uint64_t ct[kDfCt];  // recent colours: (position + 1) | word << 32, by position mod kDfCt
+    uint64_t ring[kDfQ];  // queue entry y: (y + 1) | position << 32 at y mod kDfQ, or in fr2[y]
+    uint32_t qh, qr, qp, inflight;
+};
+constexpr int kPQh = 52, kPQt = 53;  // pipe words: the queue's head and tail
+
+__global__ __launch_bounds__(1024) void sq_colour3df_kernel(SqWs w, int C, int H, int W, int e, int fin,
+                                                            uint64_t round_ticks) {
+    __shared__ C3DfLds L;
+    const int tid = threadIdx.x, g = tid / kL3, gl = tid % kL3, lane = tid & 63;
+    const Img m = image(w, blockIdx.x);
+    const int eh = m.eh, ew = m.ew;
+    (void)eh;
+    int tb[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        int a, b;
+        val_pos(gl + kL3 * k, a, b);
+        tb[k] = (a + 4) * 9 + b + 4;
+        win_pos(gl + kL3 * k, a, b);
+        tb[k] |= ((a + 4) * 9 + b + 4) << 8;
+        if (k < 4) {
+            disk_pos(gl + kL3 * k, a, b);
+            tb[k] |= ((a + 4) * 9 + b + 4) << 16;
+        }
+    }
+#define VC(k) (tb[k] & 0xFF)
+#define WC(k) ((tb[k] >> 8) & 0xFF)
+#define DC(k) (tb[k] >> 16)
+    // the queue: carried entries, then RECORD's new ready holes
+    const uint32_t q0 = m.pipe[kPRqc], q1 = m.meta[2], h0 = m.pipe[kPQh], t0q = m.pipe[kPQt];
+    for (uint32_t x = tid; x < q1 - q0; x += 1024) m.fr2[t0q + x] = m.rq[q0 + x];
+    for (int x = tid; x < kDfCt; x += 1024) L.ct[x] = 0ull;
+    for (int x = tid; x < kDfQ; x += 1024) L.ring[x] = 0ull;
+    if (tid == 0) {
+        L.qh = h0;
+        L.qr = L.qp = t0q + (q1 - q0);
+        L.inflight = 0u;
+        if (h0 < t0q + (q1 - q0)) {
+            if (m.pipe[kPCRounds] == 0u) put64(m.pipe + kPTc0, wall_clock64());
+            m.pipe[kPCRounds] += 1u;
+        }
+    }
+    sync_all();
+    const uint64_t deadline =
+        fin ? ~uint64_t(0)
+            : (uint64_t(w.pipe[kPT0]) | (uint64_t(w.pipe[kPT0 + 1]) << 32)) + round_ticks * uint64_t(e + 2);
+    const uint64_t tstart = wall_clock64();
+    const int nch = 3 * C;
+    uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    (void)prof;
+    uint32_t batches = 0;
+    for (;;) {
+        // take up to 8 entries: read their ring slots first, then claim them
+        // with a CAS on the head -- a producer overwrites the slot of entry y
+        // only once the head has passed y - kDfQ (its space check), so slots
+        // read before a successful claim hold the claimed entries or stale tags
+        uint32_t take = 0, qbase = 0;
+        uint64_t se = 0;
+        for (int t = 0; t < 64; ++t) {
+            uint32_t h = 0, pq = 0;
+            if (lane == 0) {
+                h = __hip_atomic_load(&L.qh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                pq = __hip_atomic_load(&L.qp, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            h = __shfl(h, 0);
+            pq = __shfl(pq, 0);
+            if (h >= pq) break;  // (no provisional count while the queue is empty: the "all done" test sees 0)
+            const uint32_t want = pq - h < 8u ? pq - h : 8u;
+            if (uint32_t(lane) < want)
+                se = __hip_atomic_load(&L.ring[(h + uint32_t(lane)) & uint32_t(kDfQ - 1)], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+            asm volatile("" : "+v"(se));  // read before the claim
+            uint32_t ok = 0;
+            if (lane == 0) {
+                atomicAdd(&L.inflight, 8u);  // before the take: no false "all done"
+                if (atomicCAS(&L.qh, h, h + want) == h) {
+                    ok = 1u;
+                    atomicSub(&L.inflight, 8u - want);
+                } else {
+                    atomicSub(&L.inflight, 8u);
+                }
+            }
+            if (__shfl(ok, 0)) {
+                take = want;
+                qbase = h;
+                break;
+            }
+        }
+        if (take == 0u) {
+            uint32_t quit = 0;
+            if (lane == 0) {
+                const uint64_t now = wall_clock64();
+                const uint32_t h = __hip_atomic_load(&L.qh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                const uint32_t pq = __hip_atomic_load(&L.qp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                const uint32_t inf = __hip_atomic_load(&L.inflight, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                quit = (h >= pq && inf == 0u) || now >= deadline ? 1u : 0u;
+                if (now - tstart > 400000000ull) {  // 4 s: cannot happen
+                    atomicOr(&g_sq_fault, 32u);
+                    quit = 1u;
+                }
+            }
+            if (__shfl(quit, 0)) break;
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        SQ_T(c0);
+        {
+            // keep the lane tables opaque, so the compiler does not hoist
+            // their derived offsets out of the loop (register pressure)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) asm volatile("" : "+v"(tb[k]));
+            const bool act = uint32_t(g & 7) < take;  // the wave's 8 hole slots
+            const uint32_t y = qbase + uint32_t(g & 7);
+            uint64_t ent = __shfl(se, g & 7);
+            if (act && uint32_t(ent) != y + 1u) ent = m.fr2[y];  // not in the ring: fr2 (pixel << 32 | pixel)
+            const uint32_t p = uint32_t(ent >> 32), idx = p;
+            const int i = int(p / uint32_t(ew)), j = int(p - uint32_t(i) * uint32_t(ew));
+            // the level's one round of loads
+            const uint32_t *rp = m.rec + size_t(idx) * kRecW;
+            uint4 wq = make_uint4(0, 0, 0, 0), cq = wq, mq = wq;
+            uint32_t v[8];
+            if (act) {
+                wq = *reinterpret_cast<const uint4 *>(rp + 4 * gl);
+                cq = *reinterpret_cast<const uint4 *>(rp + 32);
+                mq = *reinterpret_cast<const uint4 *>(rp + 36);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const int y = min(max(i - 5 + VC(k) / 9, 0), H - 1), x = min(max(j - 5 + VC(k) % 9, 0), W - 1);
+                    v[k] = (gl + kL3 * k < kVal3)
+                               ? __hip_atomic_load(m.shd + int64_t(y) * W + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                               : 0u;
+                }
+            }
+            SQ_T(c0a);
+            float *bf = L.buf[g];
+            uint32_t *gv = reinterpret_cast<uint32_t *>(bf);
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                if (gl + kL3 * k < kVal3) gv[VC(k)] = v[k];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // the earlier holes this one reads (RECORD's mask in the record's
+            // spare weight words 23 and 27: lanes 5 and 6 of the hole) may
+            // have released it before storing their colour: wait until each
+            // one's word carries the coloured flag (byte 3), re-reading the
+            // window past the vector L1
+            {
+                const int hl0 = (tid & 63) & ~(kL3 - 1);
+                const uint32_t elo = __shfl(wq.w, hl0 + 5), ehi = __shfl(wq.w, hl0 + 6);
+                const uint64_t em = act ? (uint64_t(elo) | (uint64_t(ehi) << 32)) : 0ull;
+                for (int tries = 0;; ++tries) {
+                    bool miss = false;
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) asm volatile("" : "+v"(tb[k]));  // no hoisted offsets (spills)
+#pragma unroll
+                    for (int k = 0; k < 8; ++k)
+                        if (gl + kL3 * k < kWin && ((em >> (gl + kL3 * k)) & 1u) && (gv[WC(k)] >> 24) == 0u) {
+                            // the workgroup's table of recent colours first
+                            const uint32_t q = p + uint32_t((WC(k) / 9 - 4) * ew + (WC(k) % 9 - 4));
+                            const uint64_t ce = __hip_atomic_load(&L.ct[q & uint32_t(kDfCt - 1)], __ATOMIC_RELAXED,
+                                                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+                            if (uint32_t(ce) == q + 1u)
+                                gv[WC(k)] = uint32_t(ce >> 32);
+                            else
+                                miss = true;
+                        }
+                    if (!__any(miss)) break;
+                    if (tries > (1 << 20)) {  // cannot happen: every released hole is being coloured
+                        if (gl == 0) atomicOr(&g_sq_fault, 32u);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    if ((tries & 7) != 7) continue;  // the table entry may have been displaced: re-read now and then
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const int y = min(max(i - 5 + VC(k) / 9, 0), H - 1), x = min(max(j - 5 + VC(k) % 9, 0), W - 1);
+                        if (act && gl + kL3 * k < kVal3)
+                            gv[VC(k)] = __hip_atomic_load(m.shd + int64_t(y) * W + x, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+            // release the later holes that read this one (their counters
+            // reach zero only after this level's barrier is passed).  Issued
+            // after the loads have landed, so no wait for the loads also
+            // waits for these: their round trip overlaps the arithmetic.
+            const uint64_t dep = uint64_t(mq.x) | (uint64_t(mq.y) << 32);
+            uint32_t old[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                old[k] = 0;
+                if (act && gl + kL3 * k < kWin && ((dep >> (gl + kL3 * k)) & 1u)) {
+                    const int64_t q = int64_t(p) + int64_t(WC(k) / 9 - 4) * ew + (WC(k) % 9 - 4);
+#if OFD_C3_PF
+                    // the dependant's record (two 128-byte lines) towards this
+                    // CU: a later level loads it (into a discarded LDS word)
+                    const uint32_t *qr = m.rec + size_t(q) * kRecW;
+                    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)qr,
+                                                     (__attribute__((address_space(3))) void *)L.dump, 4, 0, 0);
+                    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(qr + kRecW - 1),
+                                                     (__attribute__((address_space(3))) void *)L.dump, 4, 0, 0);
+#endif
+                    old[k] = atomicAdd(&m.kc[q], 1u);
+                }
+            }
+            // the holes whose last earlier neighbour this was join the queue
+            // (after this hole's colour is stored: the caller's order): slots
+            // reserved with one LDS atomic per wave, written, then published
+            // in reservation order
+            auto append_ready = [&]() {
+                asm volatile("" : "+v"(old[0]), "+v"(old[1]), "+v"(old[2]), "+v"(old[3]), "+v"(old[4]), "+v"(old[5]),
+                             "+v"(old[6]), "+v"(old[7]));
+                unsigned rmask = 0;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) rmask |= (old[k] + 1u == kK ? 1u : 0u) << k;
+                const uint32_t cnt = uint32_t(__popc(rmask));
+                const int lane = tid & 63;
+                uint32_t incl = cnt;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint32_t y = __shfl_up(incl, d);
+                    if (lane >= d) incl += y;
+                }
+                const uint32_t tot = __shfl(incl, 63);
+                if (tot == 0u) return;  // wave-uniform
+                uint32_t rb = 0, hq = 0;
+                if (lane == 63) {
+                    rb = atomicAdd(&L.qr, tot);
+                    hq = __hip_atomic_load(&L.qh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+                rb = __shfl(rb, 63);
+                hq = __shfl(hq, 63);
+                uint32_t f = rb + incl - cnt;
+                bool glob = false;
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    if (rmask & (1u << k)) {
+                        const int64_t q = int64_t(p) + int64_t(WC(k) / 9 - 4) * ew + (WC(k) % 9 - 4);
+                        if (f - hq < uint32_t(kDfQ)) {  // the slot's previous entry (f - kDfQ) is claimed
+                            __hip_atomic_store(&L.ring[f & uint32_t(kDfQ - 1)], (uint64_t(q) << 32) | uint64_t(f + 1u),
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        } else {
+                            m.fr2[f] = (uint64_t(q) << 32) | uint64_t(q);
+                            glob = true;
+                        }
+                        ++f;
+                    }
+                if (__any(glob)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the overflow's stores
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_wave_barrier();
+                if (lane == 0) {
+                    for (int t = 0; __hip_atomic_load(&L.qp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != rb; ++t) {
+                        if (t > (1 << 22)) {  // cannot happen: earlier reservations publish without waiting
+                            atomicOr(&g_sq_fault, 32u);
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                    __hip_atomic_store(&L.qp, rb + tot, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            };
+            SQ_T(c1);
+            // this lane's terms (disk positions gl + 8k): channels 1 and 2 go
+            // to LDS at once (past the grid), channel 0 waits in registers
+            // until every lane of the hole is done with the grid
+            const uint32_t wts[4] = {wq.x, wq.y, wq.z, wq.w};
+            const uint32_t cw = (gl >> 1) == 0 ? cq.x : (gl >> 1) == 1 ? cq.y : (gl >> 1) == 2 ? cq.z : cq.w;
+            const uint32_t codes = cw >> (16 * (gl & 1));
+            float t0[4][3];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int a = DC(k) / 9 - 4, b = DC(k) % 9 - 4, y = i + a, x = j + b;
+                const int k1 = y == 1, kE = y == eh - 2, l1 = x == 1, lE = x == ew - 2;
+                auto G = [&](int ry, int rx) -> uint32_t {  // colour word at window offset (ry, rx), |ry|, |rx| <= 4
+                    return gv[(ry + 4) * 9 + rx + 4];
+                };
+                const uint32_t w0 = G(a + k1, b + l1), w1 = G(a + k1, b + 1 - lE), w2 = G(a + k1, b - 1 + l1),
+                               w3 = G(a + k1, b - lE), w4 = G(a + 1 - kE, b + l1), w5 = G(a - 1 + k1, b + l1),
+                               w6 = G(a - kE, b + l1);
+                const float wt = __uint_as_float(wts[k]);
+                const uint32_t cx = (codes >> (4 * k)) & 3u, cy = (codes >> (4 * k + 2)) & 3u;
+                // cv2's gradient cases as (A - B) * f, selected once for all channels:
+                // code 0: (v1 - v2) * 2, 1: (v1 - v0), 2: (v3 - v2), 3: none ((v0 - v0) * 0 = +0)
+                const uint32_t xa = cx <= 1u ? w1 : (cx == 2u ? w3 : w0), xb = (cx & 1u) ? w0 : w2;
+                const uint32_t ya = cy <= 1u ? w4 : (cy == 2u ? w6 : w0), yb = (cy & 1u) ? w0 : w5;
+                // gix * rx = (A - B) * (f * rx) exactly: integers below 2^24 (the
+                // sign of an exact zero may differ, which no result can see)
+                const float kx = (cx == 0u ? 2.0f : (cx == 3u ? 0.0f : 1.0f)) * float(-b);
+                const float ky = (cy == 0u ? 2.0f : (cy == 3u ? 0.0f : 1.0f)) * float(-a);
+                const bool live = gl + kL3 * k < kDisk;
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    auto byte = [&](uint32_t q) -> int { return int((q >> (8 * c)) & 0xFFu); };
+                    const float vs = float(byte(w0));
+                    const float dx = float(byte(xa) - byte(xb)), dy = float(byte(ya) - byte(yb));
+                    const float ta = wt * vs, tx = wt * (dx * kx), ty = wt * (dy * ky);
+                    if (c == 0) {
+                        t0[k][0] = ta;
+                        t0[k][1] = tx;
+                        t0[k][2] = ty;
+                    } else if (live) {  // chains past 3 * C are never summed
+                        bf[(3 * c) * kDisk + gl + kL3 * k] = ta;
+                        bf[(3 * c + 1) * kDisk + gl + kL3 * k] = tx;
+                        bf[(3 * c + 2) * kDisk + gl + kL3 * k] = ty;
+                    }
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (gl + kL3 * k < kDisk)
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) bf[q * kDisk + gl + kL3 * k] = t0[k][q];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            SQ_T(c2);
+            // cv2's sums in its (k, l) order: chains gl and gl + 8 side by side
+            // (independent accumulators; Ia chains add, Jx / Jy chains subtract)
+            {
+                const int c1 = gl, c2 = gl + kL3;
+                const bool has2 = c2 < nch;
+                const float *t1 = bf + c1 * kDisk, *t2 = bf + (has2 ? c2 : c1) * kDisk;
+                const float s1 = c1 % 3 == 0 ? 1.f : -1.f, s2 = c2 % 3 == 0 ? 1.f : -1.f;
+                float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+                for (int q = 0; q < kDisk; ++q) {
+                    a1 += s1 * t1[q];  // x * +-1 is exact: acc + (-t) == acc - t
+                    a2 += s2 * t2[q];
+                }
+                if (c1 < nch) L.res[g][c1] = a1;
+                if (has2) L.res[g][c2] = a2;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            SQ_T(cb);
+#ifdef OFD_SQ_PROF
+            asm volatile("" : "+v"(old[0]), "+v"(old[1]), "+v"(old[2]), "+v"(old[3]), "+v"(old[4]), "+v"(old[5]),
+                         "+v"(old[6]), "+v"(old[7]));
+#endif
+            SQ_T(ca);
+            // queue the holes this one's releases completed now, before its
+            // colour exists: their loads overlap the rest of this hole (they
+            // wait for its coloured flag)
+            append_ready();
+            SQ_T(c3);
+            {
+                unsigned u = 0;
+                if (act && gl < C) {
+                    const float sum = __uint_as_float(mq.z);
+                    const float Ia = L.res[g][3 * gl], Jx = L.res[g][3 * gl + 1], Jy = L.res[g][3 * gl + 2];
+                    const float sat = float(double(Ia / sum) +
+                                            double(Jx + Jy) / (sqrt(double(Jx * Jx + Jy * Jy)) + double(1.0e-20f)) +
+                                            double(0.5f));
+                    u = sat_u8(sat);
+                }
+                // the hole's channels and the coloured flag in one word store
+                const int hl0 = (tid & 63) & ~(kL3 - 1);
+                const unsigned u1 = __shfl(u, hl0 + 1), u2 = __shfl(u, hl0 + 2);
+                if (act && gl == 0) {
+                    const uint32_t word = u | (u1 << 8) | (u2 << 16) | 0xFF000000u;
+                    m.shd[int64_t(i - 1) * W + (j - 1)] = word;
+                    __hip_atomic_store(&L.ct[p & uint32_t(kDfCt - 1)], (uint64_t(word) << 32) | uint64_t(p + 1u),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            SQ_T(c4);
+            SQ_ACC(2, c0, c0a);
+            SQ_ACC(6, c0a, c1);
+            SQ_ACC(3, c1, c2);
+            SQ_ACC(4, c2, cb);  // chains
+            SQ_ACC(7, cb, ca);  // the release atomics' return
+            SQ_ACC(1, ca, c3);  // the append
+            SQ_ACC(5, c3, c4);
+        }
+        if (lane == 0) atomicSub(&L.inflight, take);
+        ++batches;
+        if (__shfl(lane == 0 ? (wall_clock64() >= deadline ? 1u : 0u) : 0u, 0)) break;  // the rest is carried
+    }
+    if (lane == 0) atomicAdd(&m.meta[6], batches);
+    __syncthreads();
+    // the unclaimed entries still in the ring go to fr2 for the next round
+    for (uint32_t y = L.qh + uint32_t(tid); y < L.qp; y += 1024) {
+        const uint64_t v = L.ring[y & uint32_t(kDfQ - 1)];
+        if (uint32_t(v) == y + 1u) m.fr2[y] = (v & 0xFFFFFFFF00000000ull) | (v >> 32);
+    }
+    if (tid == 0) {
+        const uint32_t hq = L.qh, pq = L.qp;
+        if (hq >= pq && q1 + t0q > h0) put64(m.pipe + kPTc1, wall_clock64());
+        m.pipe[kPQh] = hq;
+        m.pipe[kPQt] = pq;
+        m.pipe[kPRqc] = q1;
+#ifdef OFD_SQ_PROF
+        for (int k = 0; k < 8; ++k) m.meta[16 + k] += uint32_t(prof[k] >> 8);  // wave 0's batches, all rounds
+        m.meta[7] += batches;
+#endif
+    }
+}
+#undef VC
+#undef WC
+#undef DC
+
 // Pacing of the pipelined fill's RECORD / COLOUR3 rounds (one workgroup).
 // Round e first waits -- bounded by bound_ticks -- until round_ticks * (e + 1)
 // after round 0 began, or until every image's two marches are done; then it
@@ -3000,6 +3441,10 @@ int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float 
         pipe_ticks = uint64_t(pipe_us_setting()) * uint64_t(khz) / 1000u;
     }
     const int cwk = cw_buckets_setting();
+    static const bool df_colour = [] {  // OFD_SEQ_DF=1: the levels-free colour pass (sq_colour3df_kernel)
+        const char *e = getenv("OFD_SEQ_DF");
+        return e && atoi(e) != 0;
+    }();
     // one chunk of nb images (workspace w) on stream s
     auto run_chunk = [&](const SqWs &w, int64_t b0, int64_t nb, hipStream_t s) {
         hipLaunchKernelGGL(sq_prep_tile_kernel, dim3(unsigned((W + 63) / 64), unsigned((H + 15) / 16), unsigned(nb)),
@@ -3042,8 +3487,12 @@ int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float 
         auto round = [&](hipStream_t rs, int e, int fin) {  // one RECORD / COLOUR3 round
             hipLaunchKernelGGL(sq_pace_kernel, dim3(1), dim3(256), 0, rs, w, int(nb), e, fin, pipe_ticks, 4 * pipe_ticks);
             hipLaunchKernelGGL(sq_record3_kernel, rgrid, dim3(256), 0, rs, w);
-            hipLaunchKernelGGL(sq_colour3_kernel, dim3(unsigned(nb)), dim3(1024), 0, rs, w, int(C), int(H), int(W), e,
-                               fin, pipe_ticks);
+            if (df_colour)
+                hipLaunchKernelGGL(sq_colour3df_kernel, dim3(unsigned(nb)), dim3(1024), 0, rs, w, int(C), int(H), int(W),
+                                   e, fin, pipe_ticks);
+            else
+                hipLaunchKernelGGL(sq_colour3_kernel, dim3(unsigned(nb)), dim3(1024), 0, rs, w, int(C), int(H), int(W), e,
+                                   fin, pipe_ticks);
         };
         // Pipelined (radius 3, C <= 3, large images): while the marches run
         // on s, a helper stream runs `rounds` RECORD / COLOUR3 rounds over the
