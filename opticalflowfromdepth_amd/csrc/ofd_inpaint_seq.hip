@@ -2742,6 +2742,12 @@ __global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, int C, int H, 
 // sets it on kept pixels, the colour store on holes).  A wave leaves when
 // the queue is empty and no wave holds a hole, or at the deadline (the
 // queue is carried to the next round).  Every wait is bounded (fault 32).
+#ifndef OFD_DF_SPIN  // levels-free pass: re-check only the still-missing cells while waiting
+#define OFD_DF_SPIN 0
+#endif
+#ifndef OFD_DF_SLEEP  // ... and the wait's s_sleep between checks (64 clocks per unit)
+#define OFD_DF_SLEEP 1
+#endif
 constexpr int kDfCt = 2048;  // recent-colour table entries
 constexpr int kDfQ = 512;    // queue entries held in LDS (the rest in fr2)
 struct C3DfLds {
@@ -2900,6 +2906,45 @@ __global__ __launch_bounds__(1024) void sq_colour3df_kernel(SqWs w, int C, int H
                 const int hl0 = (tid & 63) & ~(kL3 - 1);
                 const uint32_t elo = __shfl(wq.w, hl0 + 5), ehi = __shfl(wq.w, hl0 + 6);
                 const uint64_t em = act ? (uint64_t(elo) | (uint64_t(ehi) << 32)) : 0ull;
+#if OFD_DF_SPIN
+                // this lane's window cells whose earlier hole has no colour
+                // yet; only those are looked up again (a waiting wave's issue
+                // is taken from the waves that colour)
+                uint32_t pend = 0;
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    if (gl + kL3 * k < kWin && ((em >> (gl + kL3 * k)) & 1u) && (gv[WC(k)] >> 24) == 0u) pend |= 1u << k;
+                for (int tries = 0; __any(pend != 0u); ++tries) {
+                    if (tries > (1 << 20)) {  // cannot happen: every released hole is being coloured
+                        if (gl == 0) atomicOr(&g_sq_fault, 32u);
+                        break;
+                    }
+                    const bool reload = (tries & 7) == 7;  // the table entry may have been displaced
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) asm volatile("" : "+v"(tb[k]));  // no hoisted offsets (spills)
+#pragma unroll
+                    for (int k = 0; k < 8; ++k)
+                        if (pend & (1u << k)) {
+                            const uint32_t q = p + uint32_t((WC(k) / 9 - 4) * ew + (WC(k) % 9 - 4));
+                            const uint64_t ce = __hip_atomic_load(&L.ct[q & uint32_t(kDfCt - 1)], __ATOMIC_RELAXED,
+                                                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+                            uint32_t wv = uint32_t(ce >> 32);
+                            if (uint32_t(ce) != q + 1u) {
+                                wv = 0u;
+                                if (reload)  // an interior hole: no clamp
+                                    wv = __hip_atomic_load(
+                                        m.shd + int64_t(i - 5 + WC(k) / 9) * W + (j - 5 + WC(k) % 9), __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+                            }
+                            if ((wv >> 24) != 0u) {
+                                gv[WC(k)] = wv;
+                                pend &= ~(1u << k);
+                            }
+                        }
+                    if (!__any(pend != 0u)) break;
+                    __builtin_amdgcn_s_sleep(OFD_DF_SLEEP);
+                }
+#else
                 for (int tries = 0;; ++tries) {
                     bool miss = false;
 #pragma unroll
@@ -2934,6 +2979,7 @@ __global__ __launch_bounds__(1024) void sq_colour3df_kernel(SqWs w, int C, int H
                     __builtin_amdgcn_wave_barrier();
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 }
+#endif
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -3006,6 +3052,7 @@ __global__ __launch_bounds__(1024) void sq_colour3df_kernel(SqWs w, int C, int H
                 if (__any(glob)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the overflow's stores
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                 __builtin_amdgcn_wave_barrier();
+                SQ_T(cs0);
                 if (lane == 0) {
                     for (int t = 0; __hip_atomic_load(&L.qp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != rb; ++t) {
                         if (t > (1 << 22)) {  // cannot happen: earlier reservations publish without waiting
@@ -3016,6 +3063,8 @@ __global__ __launch_bounds__(1024) void sq_colour3df_kernel(SqWs w, int C, int H
                     }
                     __hip_atomic_store(&L.qp, rb + tot, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
+                SQ_T(cs1);
+                SQ_ACC(0, cs0, cs1);  // the ordered publish
             };
             SQ_T(c1);
             // this lane's terms (disk positions gl + 8k): channels 1 and 2 go

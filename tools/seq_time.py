@@ -97,8 +97,9 @@ def main():
                   "sweeps", int(r[14]))
             print("FMM (buckets > 4096 keys) -/sort/claim/push/dist/log (Mclk):",
                   [round(x * 256 / 1e6, 2) for x in r[24:30]], "sweeps", int(r[30]))
-            print("COLOUR3 level work/barrier, per-round loads/terms/chains/final+append/atomics (Mclk):",
-                  [round(x * 256 / 1e6, 2) for x in r[16:23]])
+            print("COLOUR3 level work/barrier, per-round loads/terms/chains/final+append/atomics (Mclk;"
+                  " levels-free pass: publish/append/loads/terms/chains/final/wait/atomic return):",
+                  [round(x * 256 / 1e6, 2) for x in r[16:24]])
         print("max levels", m[:, 3].max(), "max buckets", m[:, 4].max(), "errors", int((m[:, 5] != 0).sum()))
         if m[:, 8:24].any():  # per image: FMM phase sum vs COLOUR3 level work + barrier (Mclk)
             f = m[:, 8:14].astype(np.float64).sum(1) * 256 / 1e6
