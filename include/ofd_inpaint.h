@@ -127,6 +127,13 @@ int ofd_inpaint_seq_set_pipeline(int rounds, int round_us, int force);
  * Process-wide; returns the previous number of buckets. */
 int ofd_inpaint_seq_set_chipwide(int buckets, int min_pending);
 
+/* The sequential fill's colour pass: mode 1 = levels-free (a hole is
+ * coloured as soon as every earlier hole it reads is; no level barrier),
+ * 0 = level-synchronous (one workgroup barrier per Kahn level).  Results
+ * never depend on it.  Negative: leave it; default OFD_SEQ_DF (else 1).
+ * Process-wide; returns the previous mode. */
+int ofd_inpaint_seq_set_colour(int mode);
+
 /* The device whose helper streams a grouped sequential fill on `stream`
  * would use: the stream's own device (helpers are kept per device and
  * created there on first use), or -1 if it cannot be told. */

@@ -3362,7 +3362,13 @@ int pipe_us_setting() {
 #define OFD_SEQ_CW_DEFAULT 0
 #endif
 int g_cw_buckets = -1;
-uint32_t g_cw_min = kCwMinDefault;  // ofd_inpaint_seq_set_chipwide (tests: 0 keeps small marches chip-wide)
+uint32_t g_cw_min = kCwMinDefault;
+// the colour pass: 1 = levels-free (sq_colour3df_kernel), 0 = level-synchronous
+// COLOUR3; ofd_inpaint_seq_set_colour, default OFD_SEQ_DF (else 1)
+int g_df_colour = [] {
+    const char *e = getenv("OFD_SEQ_DF");
+    return e ? (atoi(e) != 0 ? 1 : 0) : 1;
+}();  // ofd_inpaint_seq_set_chipwide (tests: 0 keeps small marches chip-wide)
 int cw_buckets_setting() {
     if (g_cw_buckets < 0) {
         const char *e = getenv("OFD_SEQ_CW");
@@ -3415,6 +3421,12 @@ int ofd_inpaint_seq_helper_device(void *stream) {
     const int dev = stream_device(static_cast<hipStream_t>(stream));
     SeqHelpers *h = seq_helpers(dev);
     return h && h->ok ? h->device : -1;
+}
+
+int ofd_inpaint_seq_set_colour(int mode) {
+    const int prev = g_df_colour;
+    if (mode >= 0) g_df_colour = mode != 0 ? 1 : 0;
+    return prev;
 }
 
 int ofd_inpaint_seq_set_chipwide(int buckets, int min_pending) {
@@ -3490,10 +3502,8 @@ int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float 
         pipe_ticks = uint64_t(pipe_us_setting()) * uint64_t(khz) / 1000u;
     }
     const int cwk = cw_buckets_setting();
-    static const bool df_colour = [] {  // OFD_SEQ_DF=1: the levels-free colour pass (sq_colour3df_kernel)
-        const char *e = getenv("OFD_SEQ_DF");
-        return e && atoi(e) != 0;
-    }();
+    const bool df_colour = g_df_colour != 0;
+
     // one chunk of nb images (workspace w) on stream s
     auto run_chunk = [&](const SqWs &w, int64_t b0, int64_t nb, hipStream_t s) {
         hipLaunchKernelGGL(sq_prep_tile_kernel, dim3(unsigned((W + 63) / 64), unsigned((H + 15) / 16), unsigned(nb)),

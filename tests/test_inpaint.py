@@ -629,6 +629,57 @@ def test_inpaint_sequential_chipwide_buckets_on_warped_images(seq_chipwide):
     assert _native.lib().ofd_inpaint_faults(1) == 0
 
 
+@pytest.fixture
+def seq_colour():
+    """Sets the sequential fill's colour pass for one test
+    (ofd_inpaint_seq_set_colour) and restores it afterwards."""
+    from opticalflowfromdepth_amd import _native
+    lib = _native.lib()
+    prev = lib.ofd_inpaint_seq_set_colour(-1)
+    yield lambda mode: lib.ofd_inpaint_seq_set_colour(mode)
+    lib.ofd_inpaint_seq_set_colour(prev)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [0, 1], ids=["levels", "levels_free"])
+@pytest.mark.parametrize("case", _gpu_cases() + _seq_extra_cases(), ids=lambda c: c[0])
+def test_inpaint_sequential_colour_passes_bit_exact(case, mode, seq_colour, seq_pipeline):
+    """Both colour passes -- level-synchronous COLOUR3 and the levels-free pass
+    (a hole starts once its last earlier neighbour has released it and waits
+    for their coloured flags) -- unpipelined and in forced short rounds that
+    carry their queue: cv2's order bit for bit."""
+    from opticalflowfromdepth_amd import _native, ops
+    name, img, v, c, r = case
+    dev = torch.device("cuda:0")
+    seq_colour(mode)
+    exp = oracle.inpaint(img, v, c, r, layered=False)
+    for rounds, us, force in ((0, 2000, 0), (64, 2, 1)):
+        seq_pipeline(rounds, us, force)
+        got = ops.inpaint(torch.from_numpy(img).to(dev), torch.from_numpy(v).to(dev), torch.from_numpy(c).to(dev),
+                          radius=r, order="sequential").cpu().numpy()
+        bad = np.argwhere(got != exp)
+        assert bad.size == 0, f"{name} rounds {rounds}: {len(bad)} differing values, first {bad[:5].tolist()}"
+    assert _native.lib().ofd_inpaint_faults(1) == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [0, 1], ids=["levels", "levels_free"])
+def test_inpaint_sequential_colour_passes_on_warped_images(mode, seq_colour):
+    """Warped 768x1024 images (8 at once, pipelined by default): each colour
+    pass gives the oracle's cv2 order."""
+    from opticalflowfromdepth_amd import _native, forward_warp_flow, ops, synth
+    dev = torch.device("cuda:0")
+    seeds = [12345, 12346, 12377, 12378, 12401, 12402, 12433, 12434]
+    obj, flow, depth = synth.stage_one_batch(seeds, 768, 1024, dev)
+    out, valid, coll = forward_warp_flow(obj, flow, depth)
+    rgb = (out[:, 0:3] * valid).contiguous()
+    seq_colour(mode)
+    got = ops.inpaint(rgb, valid, coll, order="sequential").cpu().numpy()
+    exp = oracle.inpaint(rgb.cpu().numpy(), valid.cpu().numpy(), coll.cpu().numpy(), 3, layered=False)
+    assert np.array_equal(got, exp)
+    assert _native.lib().ofd_inpaint_faults(1) == 0
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("rounds,us", [(0, 2000), (12, 2000), (48, 100), (4, 5000)])
 def test_inpaint_sequential_pipeline_settings_agree_on_warped_images(rounds, us, seq_pipeline):

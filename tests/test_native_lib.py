@@ -115,6 +115,12 @@ def test_schedule_setters_are_host_state():
     assert lib.ofd_inpaint_seq_set_chipwide(999, -1) == 3  # clamps to 64
     assert lib.ofd_inpaint_seq_set_chipwide(-1, -1) == 64
     lib.ofd_inpaint_seq_set_chipwide(cw, 16384)
+    cm = lib.ofd_inpaint_seq_set_colour(-1)
+    assert cm in (0, 1)
+    assert lib.ofd_inpaint_seq_set_colour(1 - cm) == cm
+    assert lib.ofd_inpaint_seq_set_colour(5) == 1 - cm  # any nonzero: levels-free
+    assert lib.ofd_inpaint_seq_set_colour(-1) == 1
+    lib.ofd_inpaint_seq_set_colour(cm)
     g = lib.ofd_inpaint_seq_set_groups(-1)
     assert 1 <= g <= 4
     assert lib.ofd_inpaint_seq_set_groups(9) == g
