@@ -2743,7 +2743,7 @@ __global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, int C, int H, 
 // the queue is empty and no wave holds a hole, or at the deadline (the
 // queue is carried to the next round).  Every wait is bounded (fault 32).
 #ifndef OFD_DF_SPIN  // levels-free pass: re-check only the still-missing cells while waiting
-#define OFD_DF_SPIN 0
+#define OFD_DF_SPIN 1
 #endif
 #ifndef OFD_DF_SLEEP  // ... and the wait's s_sleep between checks (64 clocks per unit)
 #define OFD_DF_SLEEP 1
@@ -3100,7 +3100,9 @@ __global__ __launch_bounds__(1024) void sq_colour3df_kernel(SqWs w, int C, int H
                     auto byte = [&](uint32_t q) -> int { return int((q >> (8 * c)) & 0xFFu); };
                     const float vs = float(byte(w0));
                     const float dx = float(byte(xa) - byte(xb)), dy = float(byte(ya) - byte(yb));
-                    const float ta = wt * vs, tx = wt * (dx * kx), ty = wt * (dy * ky);
+                    // Jx / Jy terms negated: their chains subtract, and acc + (-t)
+                    // is acc - t exactly (as -1 * t), so every chain is a plain sum
+                    const float ta = wt * vs, tx = -(wt * (dx * kx)), ty = -(wt * (dy * ky));
                     if (c == 0) {
                         t0[k][0] = ta;
                         t0[k][1] = tx;
@@ -3130,12 +3132,11 @@ __global__ __launch_bounds__(1024) void sq_colour3df_kernel(SqWs w, int C, int H
                 const int c1 = gl, c2 = gl + kL3;
                 const bool has2 = c2 < nch;
                 const float *t1 = bf + c1 * kDisk, *t2 = bf + (has2 ? c2 : c1) * kDisk;
-                const float s1 = c1 % 3 == 0 ? 1.f : -1.f, s2 = c2 % 3 == 0 ? 1.f : -1.f;
                 float a1 = 0.f, a2 = 0.f;
 #pragma unroll
                 for (int q = 0; q < kDisk; ++q) {
-                    a1 += s1 * t1[q];  // x * +-1 is exact: acc + (-t) == acc - t
-                    a2 += s2 * t2[q];
+                    a1 += t1[q];  // Jx / Jy terms are stored negated
+                    a2 += t2[q];
                 }
                 if (c1 < nch) L.res[g][c1] = a1;
                 if (has2) L.res[g][c2] = a2;
