@@ -2742,6 +2742,9 @@ __global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, int C, int H, 
 // sets it on kept pixels, the colour store on holes).  A wave leaves when
 // the queue is empty and no wave holds a hole, or at the deadline (the
 // queue is carried to the next round).  Every wait is bounded (fault 32).
+#ifndef OFD_DF_WOFF  // levels-free pass: window-cell offsets from packed row / column bits
+#define OFD_DF_WOFF 1
+#endif
 #ifndef OFD_DF_SPIN  // levels-free pass: re-check only the still-missing cells while waiting
 #define OFD_DF_SPIN 1
 #endif
@@ -2765,7 +2768,9 @@ __global__ __launch_bounds__(1024) void sq_colour3df_kernel(SqWs w, int C, int H
     const int tid = threadIdx.x, g = tid / kL3, gl = tid % kL3, lane = tid & 63;
     const Img m = image(w, blockIdx.x);
     const int eh = m.eh, ew = m.ew;
+    const int wbias = 4 * ew + 4;
     (void)eh;
+    (void)wbias;
     int tb[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -2774,6 +2779,9 @@ __global__ __launch_bounds__(1024) void sq_colour3df_kernel(SqWs w, int C, int H
         tb[k] = (a + 4) * 9 + b + 4;
         win_pos(gl + kL3 * k, a, b);
         tb[k] |= ((a + 4) * 9 + b + 4) << 8;
+#if OFD_DF_WOFF
+        tb[k] |= int((uint32_t(a + 4) << 24) | (uint32_t(b + 4) << 28));  // the window cell's row / column + 4
+#endif
         if (k < 4) {
             disk_pos(gl + kL3 * k, a, b);
             tb[k] |= ((a + 4) * 9 + b + 4) << 16;
@@ -2781,7 +2789,12 @@ __global__ __launch_bounds__(1024) void sq_colour3df_kernel(SqWs w, int C, int H
     }
 #define VC(k) (tb[k] & 0xFF)
 #define WC(k) ((tb[k] >> 8) & 0xFF)
-#define DC(k) (tb[k] >> 16)
+#define DC(k) ((tb[k] >> 16) & 0xFF)
+#if OFD_DF_WOFF  // pixel offset of window cell WC(k): packed row / column, no division by 9
+#define WOFF(k) (int((uint32_t(tb[k]) >> 24) & 15u) * ew + int(uint32_t(tb[k]) >> 28) - wbias)
+#else
+#define WOFF(k) ((WC(k) / 9 - 4) * ew + (WC(k) % 9 - 4))
+#endif
     // the queue: carried entries, then RECORD's new ready holes
     const uint32_t q0 = m.pipe[kPRqc], q1 = m.meta[2], h0 = m.pipe[kPQh], t0q = m.pipe[kPQt];
     for (uint32_t x = tid; x < q1 - q0; x += 1024) m.fr2[t0q + x] = m.rq[q0 + x];
@@ -2925,7 +2938,7 @@ __global__ __launch_bounds__(1024) void sq_colour3df_kernel(SqWs w, int C, int H
 #pragma unroll
                     for (int k = 0; k < 8; ++k)
                         if (pend & (1u << k)) {
-                            const uint32_t q = p + uint32_t((WC(k) / 9 - 4) * ew + (WC(k) % 9 - 4));
+                            const uint32_t q = p + uint32_t(WOFF(k));
                             const uint64_t ce = __hip_atomic_load(&L.ct[q & uint32_t(kDfCt - 1)], __ATOMIC_RELAXED,
                                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
                             uint32_t wv = uint32_t(ce >> 32);
@@ -2953,7 +2966,7 @@ __global__ __launch_bounds__(1024) void sq_colour3df_kernel(SqWs w, int C, int H
                     for (int k = 0; k < 8; ++k)
                         if (gl + kL3 * k < kWin && ((em >> (gl + kL3 * k)) & 1u) && (gv[WC(k)] >> 24) == 0u) {
                             // the workgroup's table of recent colours first
-                            const uint32_t q = p + uint32_t((WC(k) / 9 - 4) * ew + (WC(k) % 9 - 4));
+                            const uint32_t q = p + uint32_t(WOFF(k));
                             const uint64_t ce = __hip_atomic_load(&L.ct[q & uint32_t(kDfCt - 1)], __ATOMIC_RELAXED,
                                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
                             if (uint32_t(ce) == q + 1u)
@@ -2994,7 +3007,7 @@ __global__ __launch_bounds__(1024) void sq_colour3df_kernel(SqWs w, int C, int H
             for (int k = 0; k < 8; ++k) {
                 old[k] = 0;
                 if (act && gl + kL3 * k < kWin && ((dep >> (gl + kL3 * k)) & 1u)) {
-                    const int64_t q = int64_t(p) + int64_t(WC(k) / 9 - 4) * ew + (WC(k) % 9 - 4);
+                    const int64_t q = int64_t(p) + int64_t(WOFF(k));
 #if OFD_C3_PF
                     // the dependant's record (two 128-byte lines) towards this
                     // CU: a later level loads it (into a discarded LDS word)
@@ -3039,7 +3052,7 @@ __global__ __launch_bounds__(1024) void sq_colour3df_kernel(SqWs w, int C, int H
 #pragma unroll
                 for (int k = 0; k < 8; ++k)
                     if (rmask & (1u << k)) {
-                        const int64_t q = int64_t(p) + int64_t(WC(k) / 9 - 4) * ew + (WC(k) % 9 - 4);
+                        const int64_t q = int64_t(p) + int64_t(WOFF(k));
                         if (f - hq < uint32_t(kDfQ)) {  // the slot's previous entry (f - kDfQ) is claimed
                             __hip_atomic_store(&L.ring[f & uint32_t(kDfQ - 1)], (uint64_t(q) << 32) | uint64_t(f + 1u),
                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -3213,6 +3226,7 @@ __global__ __launch_bounds__(1024) void sq_colour3df_kernel(SqWs w, int C, int H
 #undef VC
 #undef WC
 #undef DC
+#undef WOFF
 
 // Pacing of the pipelined fill's RECORD / COLOUR3 rounds (one workgroup).
 // Round e first waits -- bounded by bound_ticks -- until round_ticks * (e + 1)
