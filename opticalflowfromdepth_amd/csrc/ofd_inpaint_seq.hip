@@ -2745,6 +2745,14 @@ __global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, int C, int H, 
 #ifndef OFD_DF_WOFF  // levels-free pass: window-cell offsets from packed row / column bits
 #define OFD_DF_WOFF 1
 #endif
+#ifndef OFD_DF_A32  // levels-free pass: per-image indices in 32 bits (no 64-bit multiply-adds)
+#define OFD_DF_A32 1
+#endif
+#if OFD_DF_A32
+#define IX32(e) uint32_t(e)
+#else
+#define IX32(e) int64_t(e)
+#endif
 #ifndef OFD_DF_SPIN  // levels-free pass: re-check only the still-missing cells while waiting
 #define OFD_DF_SPIN 1
 #endif
@@ -2897,7 +2905,7 @@ __global__ __launch_bounds__(1024) void sq_colour3df_kernel(SqWs w, int C, int H
                 for (int k = 0; k < 8; ++k) {
                     const int y = min(max(i - 5 + VC(k) / 9, 0), H - 1), x = min(max(j - 5 + VC(k) % 9, 0), W - 1);
                     v[k] = (gl + kL3 * k < kVal3)
-                               ? __hip_atomic_load(m.shd + int64_t(y) * W + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                               ? __hip_atomic_load(m.shd + IX32(y * W + x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                : 0u;
                 }
             }
@@ -2946,7 +2954,7 @@ __global__ __launch_bounds__(1024) void sq_colour3df_kernel(SqWs w, int C, int H
                                 wv = 0u;
                                 if (reload)  // an interior hole: no clamp
                                     wv = __hip_atomic_load(
-                                        m.shd + int64_t(i - 5 + WC(k) / 9) * W + (j - 5 + WC(k) % 9), __ATOMIC_RELAXED,
+                                        m.shd + IX32((i - 5 + WC(k) / 9) * W + (j - 5 + WC(k) % 9)), __ATOMIC_RELAXED,
                                         __HIP_MEMORY_SCOPE_AGENT);
                             }
                             if ((wv >> 24) != 0u) {
@@ -2985,7 +2993,7 @@ __global__ __launch_bounds__(1024) void sq_colour3df_kernel(SqWs w, int C, int H
                     for (int k = 0; k < 8; ++k) {
                         const int y = min(max(i - 5 + VC(k) / 9, 0), H - 1), x = min(max(j - 5 + VC(k) % 9, 0), W - 1);
                         if (act && gl + kL3 * k < kVal3)
-                            gv[VC(k)] = __hip_atomic_load(m.shd + int64_t(y) * W + x, __ATOMIC_RELAXED,
+                            gv[VC(k)] = __hip_atomic_load(m.shd + IX32(y * W + x), __ATOMIC_RELAXED,
                                                           __HIP_MEMORY_SCOPE_AGENT);
                     }
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -3007,7 +3015,7 @@ __global__ __launch_bounds__(1024) void sq_colour3df_kernel(SqWs w, int C, int H
             for (int k = 0; k < 8; ++k) {
                 old[k] = 0;
                 if (act && gl + kL3 * k < kWin && ((dep >> (gl + kL3 * k)) & 1u)) {
-                    const int64_t q = int64_t(p) + int64_t(WOFF(k));
+                    const auto q = IX32(p + uint32_t(WOFF(k)));
 #if OFD_C3_PF
                     // the dependant's record (two 128-byte lines) towards this
                     // CU: a later level loads it (into a discarded LDS word)
@@ -3052,7 +3060,7 @@ __global__ __launch_bounds__(1024) void sq_colour3df_kernel(SqWs w, int C, int H
 #pragma unroll
                 for (int k = 0; k < 8; ++k)
                     if (rmask & (1u << k)) {
-                        const int64_t q = int64_t(p) + int64_t(WOFF(k));
+                        const auto q = IX32(p + uint32_t(WOFF(k)));
                         if (f - hq < uint32_t(kDfQ)) {  // the slot's previous entry (f - kDfQ) is claimed
                             __hip_atomic_store(&L.ring[f & uint32_t(kDfQ - 1)], (uint64_t(q) << 32) | uint64_t(f + 1u),
                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
