@@ -59,6 +59,9 @@ import torch
 REF = os.environ.get("OFD_REFERENCE", "/root/reference")
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
+# where the fixtures are written (tests/golden by default; tests/golden/check_regen.py
+# regenerates into a temporary directory and compares with the committed files)
+OUT = os.environ.get("OFD_GOLDEN_OUT", HERE)
 sys.path.insert(0, REPO)
 
 from oracle import oracle  # noqa: E402  (test infrastructure)
@@ -632,9 +635,6 @@ def make_ppa_fill_cases(utils_mod, ref_fw, Convert, h=32, w=40, seeds=(5150, 515
                     cases[f"{pre}/{nm}_val"] = flow.reshape(-1)[idx]
             cap["ego"].clear()
             cap["rot"].clear()
-    if store_flows:
-        Convert.depth_to_random_flow = staticmethod(d2rf)
-        SF._rotate, SF.forward = sf_rot, sf_fwd
         for key, (arr, kind) in files.items():
             pre = f"i{n}/{key}"
             cases[pre + "/dtype"] = np.array(arr.dtype.str)
@@ -649,6 +649,9 @@ def make_ppa_fill_cases(utils_mod, ref_fw, Convert, h=32, w=40, seeds=(5150, 515
                 else:
                     cases[f"{pre}/tolsum{c}"] = np.array([arr[c].astype(np.float64).sum(),
                                                          np.abs(arr[c].astype(np.float64)).sum()])
+    if store_flows:
+        Convert.depth_to_random_flow = staticmethod(d2rf)
+        SF._rotate, SF.forward = sf_rot, sf_fwd
     return cases
 
 
@@ -691,8 +694,8 @@ def make_loss_cases():
 def main():
     if sys.argv[1:] == ["losses"]:  # only the training-loss fixture
         lc = make_loss_cases()
-        np.savez_compressed(os.path.join(HERE, "losses.npz"), **lc)
-        print("losses.npz", os.path.getsize(os.path.join(HERE, "losses.npz")), "bytes")
+        np.savez_compressed(os.path.join(OUT, "losses.npz"), **lc)
+        print("losses.npz", os.path.getsize(os.path.join(OUT, "losses.npz")), "bytes")
         return
     ref_fw = load_reference_fw()
     geometry_mod = load_reference_geometry()
@@ -701,45 +704,45 @@ def main():
 
     if sys.argv[1:] == ["config1"]:  # only the config-1 fixture (the others are unchanged)
         c1 = make_config1_cases(ref_fw, Convert, utils_mod)
-        np.savez_compressed(os.path.join(HERE, "config1.npz"), **c1)
-        print("config1.npz", os.path.getsize(os.path.join(HERE, "config1.npz")), "bytes")
+        np.savez_compressed(os.path.join(OUT, "config1.npz"), **c1)
+        print("config1.npz", os.path.getsize(os.path.join(OUT, "config1.npz")), "bytes")
         return
     if sys.argv[1:] == ["ppa_fill"]:  # only the forward fixture with the real (oracle-Telea) fill
         pf = make_ppa_fill_cases(utils_mod, ref_fw, Convert)
-        np.savez_compressed(os.path.join(HERE, "ppa_fill.npz"), **pf)
-        print("ppa_fill.npz", os.path.getsize(os.path.join(HERE, "ppa_fill.npz")), "bytes")
+        np.savez_compressed(os.path.join(OUT, "ppa_fill.npz"), **pf)
+        print("ppa_fill.npz", os.path.getsize(os.path.join(OUT, "ppa_fill.npz")), "bytes")
         return
     if sys.argv[1:] == ["ppa_fill_large"]:  # one 192x256 image: ego-motion border bands, larger fills
         pf = make_ppa_fill_cases(utils_mod, ref_fw, Convert, h=192, w=256, seeds=(5160,), sample=(8, 8),
                                  tol_full=False, store_flows=True)
-        np.savez_compressed(os.path.join(HERE, "ppa_fill_large.npz"), **pf)
-        print("ppa_fill_large.npz", os.path.getsize(os.path.join(HERE, "ppa_fill_large.npz")), "bytes")
+        np.savez_compressed(os.path.join(OUT, "ppa_fill_large.npz"), **pf)
+        print("ppa_fill_large.npz", os.path.getsize(os.path.join(OUT, "ppa_fill_large.npz")), "bytes")
         return
     if sys.argv[1:] == ["ppa_forward"]:  # only the per-image forward fixture
         ref_inpaint, rec = load_reference_inpaint()
         utils_mod.inpaint = lambda img, valid, coll: ref_inpaint(img.as_subclass(_CpuImage), valid, coll).as_subclass(
             torch.Tensor)
         pf = make_ppa_forward_cases(utils_mod, ref_fw, Convert)
-        np.savez_compressed(os.path.join(HERE, "ppa_forward.npz"), **pf)
-        print("ppa_forward.npz", os.path.getsize(os.path.join(HERE, "ppa_forward.npz")), "bytes")
+        np.savez_compressed(os.path.join(OUT, "ppa_forward.npz"), **pf)
+        print("ppa_forward.npz", os.path.getsize(os.path.join(OUT, "ppa_forward.npz")), "bytes")
         return
     op = make_op_cases()
-    np.savez_compressed(os.path.join(HERE, "fw_op.npz"), **op)
+    np.savez_compressed(os.path.join(OUT, "fw_op.npz"), **op)
     wr = make_wrapper_cases(ref_fw)
-    np.savez_compressed(os.path.join(HERE, "fw_wrapper.npz"), **wr)
+    np.savez_compressed(os.path.join(OUT, "fw_wrapper.npz"), **wr)
     pl = make_pipeline_cases(ref_fw, Plausible, Convert, utils_mod)
-    np.savez_compressed(os.path.join(HERE, "pipeline.npz"), **pl)
+    np.savez_compressed(os.path.join(OUT, "pipeline.npz"), **pl)
     ref_inpaint, rec = load_reference_inpaint()
     im = make_inpaint_mask_cases(ref_inpaint, rec)
-    np.savez_compressed(os.path.join(HERE, "inpaint_mask.npz"), **im)
+    np.savez_compressed(os.path.join(OUT, "inpaint_mask.npz"), **im)
     # utils with inpaint = the reference's, behind the CPU-device shim
     utils_mod.inpaint = lambda img, valid, coll: ref_inpaint(img.as_subclass(_CpuImage), valid, coll).as_subclass(
         torch.Tensor)
     ns = load_reference_preprocess_slices(utils_mod, ref_fw, Convert)
     au = make_augment_cases(ns, utils_mod)
-    np.savez_compressed(os.path.join(HERE, "augment.npz"), **au)
+    np.savez_compressed(os.path.join(OUT, "augment.npz"), **au)
     for f in ("fw_op.npz", "fw_wrapper.npz", "pipeline.npz", "inpaint_mask.npz", "augment.npz"):
-        print(f, os.path.getsize(os.path.join(HERE, f)), "bytes")
+        print(f, os.path.getsize(os.path.join(OUT, f)), "bytes")
 
 
 if __name__ == "__main__":

@@ -281,6 +281,27 @@ def _check_file_vs_fill_fixture(z, pre, arr, kind=None):
                                  f"sample got {got.ravel()[:6]} exp {samp.ravel()[:6]}")
 
 
+@pytest.mark.parametrize("name", ["ppa_fill", "ppa_fill_large"])
+def test_fill_fixtures_hold_every_key_the_gpu_checks_read(name):
+    """Every i{n}/{file}/digest (and dtype, shape, sample, type) that
+    _check_dir_vs_fill_fixture reads is in the committed fixture, for every
+    seed it holds.  Round 5's make_golden.py wrote them for the last image
+    only, and only with store_flows; tests/golden/check_regen.py
+    (profiles/r06_golden_regen.txt) shows the repaired script regenerates both
+    fixtures member for member."""
+    z = np.load(os.path.join(REPO, "tests", "golden", name + ".npz"))
+    files = set(z.files)
+    keys = ["group"] + [f"{g}_{a}_{k}" for g in range(5) for a in range(12) for k in (1, 2)]
+    assert len(z["seeds"]) >= 1 and "sample_stride" in files
+    for n in range(len(z["seeds"])):
+        assert f"i{n}/holes" in files
+        for key in keys:
+            pre = f"i{n}/{key}"
+            for leaf in ("dtype", "shape", "digest", "sample") + (() if key == "group" else ("type",)):
+                assert f"{pre}/{leaf}" in files, f"{name}: {pre}/{leaf} missing"
+            assert len(z[pre + "/digest"]) == int(z[pre + "/shape"][0]), pre
+
+
 def _check_dir_vs_fill_fixture(z, n, out):
     from opticalflowfromdepth_amd import preprocess as pp
     assert sorted(os.listdir(out)) == sorted(["group.npz"] + [f"{g}_{a}_{k}.npz" for g in range(5)
