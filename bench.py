@@ -356,7 +356,7 @@ def fused_ego_phase(B, H, W, steps, dev, stream):
                 "parity": "bit-exact vs FW on the materialised concatenation (tests/test_flow_cat.py)"},
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(gbs / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_px": 52},
-            "parity": "bit-exact vs FW on ego_flow's plane; flow within 8 ulp of the reference's (tests/test_ego.py)"}
+            "parity": "bit-exact vs FW on ego_flow's plane; the plane bit-exact vs the reference's CPU run (tests/test_ego.py)"}
 
 
 def bf16_warp_phase(B, H, W, steps, dev, stream):
@@ -561,8 +561,8 @@ def main(argv=None):
 
     stream = torch.cuda.current_stream(dev)
     mk = lambda: [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    starts, ends, rstarts, rends = mk(), mk(), mk(), mk()
-    for ev in rstarts + rends:  # torch creates events lazily: force the HIP handles to exist
+    starts, ends, rstarts, rends, bstarts = mk(), mk(), mk(), mk(), mk()
+    for ev in rstarts + rends + bstarts:  # torch creates events lazily: force the HIP handles to exist
         ev.record(stream)
     torch.cuda.synchronize()
     lib = _native.lib()
@@ -585,8 +585,10 @@ def main(argv=None):
         if evmode >= 1:
             if k in sampled:
                 lib.ofd_fw_set_profile_events(rstarts[k].cuda_event, rends[k].cuda_event)
+                lib.ofd_fw_set_profile_bin_event(bstarts[k].cuda_event)
             else:
                 lib.ofd_fw_set_profile_events(None, None)
+                lib.ofd_fw_set_profile_bin_event(None)
         if evmode >= 2:
             starts[k].record(stream)
         forward_warp_flow(obj, flow, depth, out=out)
@@ -597,10 +599,15 @@ def main(argv=None):
         dist.barrier()
     wall = time.perf_counter() - t0
     lib.ofd_fw_set_profile_events(None, None)
+    lib.ofd_fw_set_profile_bin_event(None)
     ev_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)] if evmode >= 2 else [wall * 1e3 / args.steps]
     dev_ms = sum(ev_ms) / len(ev_ms)
     rv_ms = [rstarts[k].elapsed_time(rends[k]) for k in sampled] if evmode >= 1 else [dev_ms]
     resolve_ms = sum(rv_ms) / len(rv_ms)
+    bin_ms = None
+    if evmode >= 1 and args.engine != "atomic" and sampled:
+        bv = [bstarts[k].elapsed_time(rstarts[k]) for k in sampled]
+        bin_ms = sum(bv) / len(bv)
 
     ranks = rank_report(wall / args.steps * 1e3, world, coll_dev)
     t = torch.tensor([wall, dev_ms], dtype=torch.float64, device=coll_dev)
@@ -612,31 +619,54 @@ def main(argv=None):
     bytes_per_px = (2 * C + 5) * 4  # algorithmic: obj C + flow 2 + depth in; out C + valid + coll
     value = n_total * H * W * args.steps / wall / 1e6
     achieved_gbs = px_step_rank * bytes_per_px / (dev_ms / 1e3) / 1e9
-    # dominant kernel and its algorithmic bytes per source pixel:
-    #   tile  : SPLAT reads flow, depth and obj, writes output, valid and
-    #           collision -- every algorithmic byte of the op, (2C+5)*4
-    #           (BIN's flow read is the one re-read)
+    # dominant kernel and the bytes it moves per source pixel (its own, not
+    # the op's: the split of the op's 68 B/px between the launches)
+    #   tile  : SPLAT.  With BIN's packed targets (the default for a flow) it
+    #           reads obj C*4 (the winners' gather), depth 4 and the 2-byte
+    #           target code, and writes output C*4, valid 4, collision 4;
+    #           BIN reads the flow (8) and writes the code (2).  Unpacked,
+    #           SPLAT re-reads the flow itself: (2C+5)*4, every byte of the op.
     #   split : RESOLVE gathers obj and writes the C output planes, 2C*4
     #   atomic: the resolve pass also writes valid / collision, (2C+2)*4
-    kern_bpp, kern_name = {"tile": ((2 * C + 5) * 4, "splat_persist_kernel"),
+    packed = args.engine == "tile" and lib.ofd_fw_set_pack(-1) == 1
+    splat_bpp = (8 * C + 14) if packed else (2 * C + 5) * 4
+    bin_bpp = 10 if packed else 8
+    kern_bpp, kern_name = {"tile": (splat_bpp, "splat_persist_kernel"),
                            "split": (2 * C * 4, "resolve2d_kernel"),
                            "atomic": ((2 * C + 2) * 4, "resolve_atomic_kernel")}[args.engine]
     kern_gbs = px_step_rank * kern_bpp / (resolve_ms / 1e3) / 1e9
+    bin_rec = None
+    if bin_ms is not None:
+        bin_gbs = px_step_rank * bin_bpp / (bin_ms / 1e3) / 1e9
+        bin_rec = {"kernel": "bin_kernel", "event_ms_per_launch": round(bin_ms, 4), "bytes_per_px": bin_bpp,
+                   "bytes": "flow 8 in" + (", target code 2 out" if packed else ""),
+                   "achieved": round(bin_gbs, 1), "frac": round(bin_gbs / HBM_PEAK_GBS, 4)}
 
-    traffic = traffic_step = None
-    traffic_note = None
+    # PMC traffic (profiles/pmc_traffic.json, tools/profile_round.sh): only
+    # for the build that was profiled -- a file from other sources says
+    # nothing about this library's traffic
+    traffic = traffic_step = bin_traffic = None
+    traffic_note = "no PMC file for this configuration"
     pmc_file = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc_file) and args.engine != "atomic":
         try:
             pm = json.load(open(pmc_file))
             if pm.get("config") == [B, C, H, W] and pm.get("engine", "split") == args.engine:
-                traffic_step = pm.get("hbm_bytes_per_step")
-                for kk in pm.get("kernels", []):
-                    if kk["kernel"] == kern_name:
-                        traffic = kk["fetch_bytes_x2"] + kk["write_bytes"]
-                traffic_note = pm.get("source")
-        except Exception:
-            pass
+                if pm.get("build_id") != _native.build_id():
+                    traffic_note = (f"null: profiles/pmc_traffic.json is from build {pm.get('build_id')}, "
+                                    f"this run is build {_native.build_id()}")
+                else:
+                    traffic_step = pm.get("hbm_bytes_per_step")
+                    for kk in pm.get("kernels", []):
+                        if kk["kernel"] == kern_name:
+                            traffic = kk["fetch_bytes_x2"] + kk["write_bytes"]
+                        if kk["kernel"] == "bin_kernel":
+                            bin_traffic = kk["fetch_bytes_x2"] + kk["write_bytes"]
+                    traffic_note = f"profiles/pmc_traffic.json (build {pm.get('build_id')}): " + str(pm.get("source"))
+        except Exception as e:  # a malformed file is reported, not fatal
+            traffic_note = f"null: profiles/pmc_traffic.json unreadable ({e})"
+    if bin_rec is not None:
+        bin_rec["traffic"] = bin_traffic
 
     cpu = None
     threads = args.cpu_threads if args.cpu_threads > 0 else min(16, os.cpu_count() or 1)
@@ -697,7 +727,10 @@ def main(argv=None):
                          "algorithmic_bytes_per_px": kern_bpp,
                          "event_ms_per_launch": round(resolve_ms, 4),
                          "event_launches": len(sampled) if evmode >= 1 else 0,
-                         "traffic_source": traffic_note},
+                         "traffic_source": traffic_note,
+                         "bytes": (f"obj {4 * C} (winners' gather) + depth 4 + target code 2 in, output {4 * C} "
+                                   f"+ valid 4 + collision 4 out" if packed and args.engine == "tile" else None)},
+            "bin": bin_rec,
             "op_roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS,
                             "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
                             "traffic": traffic_step,

@@ -129,6 +129,12 @@ int ofd_fw_set_pack(int on);
  * wide, not thread-safe; for timing only. */
 int ofd_fw_set_profile_events(void *start_event, void *stop_event);
 
+/* Benchmark hook beside ofd_fw_set_profile_events: when non-NULL, the given
+ * hipEvent_t is recorded right before the first chunk's BIN launch (TILE
+ * engines), so BIN's duration is this event to the start event above.  NULL
+ * disables it.  Process-wide, not thread-safe; for timing only. */
+int ofd_fw_set_profile_bin_event(void *bin_start_event);
+
 /* Human-readable name of a return code (static storage). */
 const char *ofd_fw_strerror(int code);
 

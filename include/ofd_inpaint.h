@@ -149,7 +149,9 @@ int ofd_inpaint_set_schedule(int launch_layers, int thin_cap);
 /* Test / debug hook: the OR of the invariant-violation bits any hole-fill
  * kernel raised since the last reset -- 2: a sequential-march bucket index
  * passed its bound; 4: a sequential distance sweep passed its iteration bound;
- * 8: the layered fill's deep tail gave up waiting for a previous layer.  Each is unreachable while the
+ * 8: the layered fill's deep tail gave up waiting for a previous layer;
+ * 32: a bounded wait of the sequential fill's levels-free colour pass gave
+ * up (a neighbour's colour or the ready queue).  Each is unreachable while the
  * algorithm's invariants hold, and each means that call's output is
  * incomplete.  Blocking (a device-to-host copy of the fault words); reset != 0
  * clears them.  Returns the bits (>= 0) or -1 on a HIP error. */

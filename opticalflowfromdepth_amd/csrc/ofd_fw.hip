@@ -71,10 +71,13 @@ constexpr unsigned int IDX_NONE = ~0u;
 #define OFD_PROBE_TH 32
 #endif
 constexpr int TW = OFD_PROBE_TW, TH = OFD_PROBE_TH;  // target tile (LDS z-buffer 32 KiB)
-// Only the 128 x 32 tile is supported since the packed targets (round 5): a
-// 128 x 16 probe build faulted on the GPU (illegal address), so other shapes
-// no longer compile.
-static_assert(TW == 128 && TH == 32, "tile engine: 128 x 32 tiles only");
+// Tile-shape invariants are asserted where they are used: the packed target's
+// 12-bit offset (pack_target) and the fused publish's rounds (splat_tile: every
+// thread takes kGT targets per round, so TW * TH must be a multiple of
+// threads x kGT).  Round 5's 128 x 16 probe build broke the latter -- 2048
+// targets, 512 threads x 8 in flight -- and its publish read past the LDS
+// z-buffer into the block list, gathering obj at garbage winner indices
+// (the illegal address it faulted on).
 constexpr int SBW = 16, SBH = 4;          // source block = one wave (64 px)
 constexpr int SEGB = 8;                   // source blocks per segment (128 x 4 px)
 constexpr int MAX_TILES_PER_BLOCK = 12;   // wider boxes go through the global path
@@ -1252,6 +1255,7 @@ __device__ __forceinline__ void splat_tile(TileLds &L, unsigned lin, int bl, int
         // depth -- while those gathers are in flight.  Output channel c is
         // obj channel c below gen_at, generated c - gen_at, then obj c - kGen.
         constexpr int kT = Cfg::kGT, kCh = 4, kG = Coords::kGen;
+        static_assert((TW * TH) % (Cfg::kThr * kT) == 0, "publish rounds must tile the z-buffer exactly");
         const int C = io.C, Cobj = io.Cobj, ga = io.gen_at;
         const float *ob = static_cast<const float *>(io.obj) + b * int64_t(Cobj) * HW;
         float *oo = static_cast<float *>(io.out) + b * int64_t(C) * HW;
@@ -1336,6 +1340,7 @@ __device__ __forceinline__ void splat_tile(TileLds &L, unsigned lin, int bl, int
         // selects a source value, so no rounding happens anywhere)
         static_assert(Coords::kGen == 0, "generated channels take the branch above");
         constexpr int kT = Cfg::kGT, kCh = 8;
+        static_assert((TW * TH) % (Cfg::kThr * kT) == 0, "publish rounds must tile the z-buffer exactly");
         const int C = io.C;
         const E *ob = static_cast<const E *>(io.obj) + b * int64_t(io.Cobj) * HW;
         E *oo = static_cast<E *>(io.out) + b * int64_t(C) * HW;
@@ -1380,6 +1385,7 @@ __device__ __forceinline__ void splat_tile(TileLds &L, unsigned lin, int bl, int
         }
     } else {
         unsigned int *win = ws.winner + int64_t(bl) * HW;
+        static_assert((TW * TH) % Cfg::kThr == 0, "publish rounds must tile the z-buffer exactly");
 #pragma unroll
         for (int k = 0; k < TW * TH / Cfg::kThr; ++k) {
             const int q = int(threadIdx.x) + k * Cfg::kThr;
@@ -1423,13 +1429,16 @@ using SplitCfg = SplatCfg<512, 2, 8>;  // split engine: 4 workgroups / CU, light
 #ifndef OFD_PROBE_UF  // 4-block splat slots in flight per wave (probe builds override)
 #define OFD_PROBE_UF kSplatU
 #endif
-using FusedCfg = SplatCfg<OFD_PROBE_THR, OFD_PROBE_GT, OFD_PROBE_MINW, OFD_PROBE_UF>;
+// targets in flight per thread, at most the tile's targets per thread (a
+// 128 x 16 tile at 512 threads holds 4 per thread)
+constexpr int gt_cap(int gt, int thr) { return gt < TW * TH / thr ? gt : TW * TH / thr; }
+using FusedCfg = SplatCfg<OFD_PROBE_THR, gt_cap(OFD_PROBE_GT, OFD_PROBE_THR), OFD_PROBE_MINW, OFD_PROBE_UF>;
 // coordinate sources that generate channels carry the generated values and a
 // division per source: 4 targets in flight keeps them inside 128 VGPRs
 // (Coords::kGenGT of them: 4 for the disparity source, 2 for the ego-motion
 // source, whose per-target projection is the heavier)
 template <typename Coords>
-using FusedGenCfg = SplatCfg<512, Coords::kGenGT, 4>;
+using FusedGenCfg = SplatCfg<512, gt_cap(Coords::kGenGT, 512), 4>;
 template <typename Coords>
 using FusedCfgFor = typename std::conditional<Coords::kGen == 0, FusedCfg, FusedGenCfg<Coords>>::type;
 
@@ -1776,6 +1785,7 @@ unsigned persist_min() {
 // launch of a call -- the dominant kernel -- so a benchmark can time it with
 // HIP events on the stream it runs on.
 hipEvent_t g_prof_start = nullptr, g_prof_stop = nullptr;
+hipEvent_t g_prof_bin = nullptr;  // ofd_fw_set_profile_bin_event: before the first BIN
 
 // E: the obj / output element type -- float, or unsigned short for bf16
 // planes (fused TILE engine only, like coordinate sources that generate
@@ -1842,6 +1852,7 @@ int run_f32(Coords co, const E *obj, const float *depth, E *out, float *valid, f
                 using Cfg = FusedCfgFor<Coords>;
                 auto fused = [&](auto vec_c, auto pack_c) {
                     constexpr bool kV = decltype(vec_c)::value, kP = decltype(pack_c)::value;
+                    if (c == 0 && g_prof_bin) (void)hipEventRecord(g_prof_bin, st);
                     hipLaunchKernelGGL((bin_kernel<Coords, kV, kBinSPW, kP>), bgrid, dim3(kWarpThreads), 0, st, co,
                                        depth, a, int(H), int(W), HW, g);
                     if (c == 0 && g_prof_start) (void)hipEventRecord(g_prof_start, st);
@@ -2032,6 +2043,11 @@ const char *ofd_fw_build_id(void) { return OFD_BUILD_ID; }
 int ofd_fw_set_profile_events(void *start_event, void *stop_event) {
     g_prof_start = static_cast<hipEvent_t>(start_event);
     g_prof_stop = static_cast<hipEvent_t>(stop_event);
+    return OFD_FW_OK;
+}
+
+int ofd_fw_set_profile_bin_event(void *bin_start_event) {
+    g_prof_bin = static_cast<hipEvent_t>(bin_start_event);
     return OFD_FW_OK;
 }
 

@@ -1416,7 +1416,7 @@ int ofd_inpaint_faults(int reset) {
     }
     const unsigned q = ofd_sq_fault_read(reset);
     if (q == ~0u) return -1;
-    return int(v | (q & 6u));
+    return int(v | (q & (2u | 4u | 32u)));
 }
 
 int ofd_inpaint_set_schedule(int launch_layers, int thin_cap) {

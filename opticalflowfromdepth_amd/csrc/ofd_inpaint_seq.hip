@@ -63,7 +63,9 @@
 // Fault bits of the sequential fill (ofd_inpaint_faults): 2 = a march bucket
 // index past its bound, 4 = a distance sweep past its iteration bound (both
 // unreachable while the margin argument holds; the kernel stops early and the
-// output is incomplete, so a set bit means a wrong result).
+// output is incomplete, so a set bit means a wrong result), 32 = a bounded
+// wait of the levels-free colour pass gave up (a hole may then be coloured
+// from uncoloured neighbours, or left unfilled).
 __device__ unsigned g_sq_fault;
 
 namespace {
@@ -2731,7 +2733,9 @@ __global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, int C, int H, 
 #undef DC
 
 
-// COLOUR3 without levels (OFD_SEQ_DF=1, opt-in): the ready holes sit in a
+// COLOUR3 without levels (the default colour pass since round 5;
+// ofd_inpaint_seq_set_colour(0) / OFD_SEQ_DF=0 select the level-synchronous
+// COLOUR3 above): the ready holes sit in a
 // queue (fr2, positions carried across rounds in kPQh / kPQt); each wave
 // takes up to 8 of them, colours them with COLOUR3's per-hole code, and
 // queues the holes its releases completed -- no workgroup barrier, so a

@@ -304,6 +304,19 @@ def inpaint(img: torch.Tensor, valid: torch.Tensor, collision: torch.Tensor, rad
     return out[0] if squeeze else out
 
 
+def inpaint_faults(reset: bool = True) -> int:
+    """The hole-fill's invariant-violation bits since the last reset
+    (include/ofd_inpaint.h ofd_inpaint_faults: 2 / 4 a march bound, 8 the
+    layered tail's wait, 32 a wait of the levels-free colour pass).  Any set
+    bit means some fill since the reset is incomplete.  Blocking: a
+    device-to-host copy of the fault words, so callers check once per batch,
+    not per fill."""
+    rc = int(_native.lib().ofd_inpaint_faults(1 if reset else 0))
+    if rc < 0:
+        raise RuntimeError("ofd_inpaint_faults: HIP error reading the fault words")
+    return rc
+
+
 def warp_disparity(obj: torch.Tensor, depth: torch.Tensor, s: torch.Tensor,
                    out: Tuple[torch.Tensor, torch.Tensor, torch.Tensor] = None
                    ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:

@@ -112,8 +112,8 @@ class Convert:
         if T.shape[0] != d.shape[0]:
             T = T.expand(d.shape[0], 4, 4)
         if d.is_cuda:
-            # the one-kernel flow plane (ops.ego_flow, within 8 ulp of the
-            # reference's arithmetic: tests/test_ego.py)
+            # the one-kernel flow plane (ops.ego_flow, bit-exact vs the
+            # reference's CPU run: tests/test_ego.py; vs its CUDA run unpinned)
             P, ik = synth.projection(d.shape[-2], d.shape[-1], T, d.device)
             flow = ego_flow(d.contiguous(), P, ik)
         else:
@@ -551,6 +551,7 @@ class PreprocessPlusAugment(nn.Module):
                     save_augment(out_dirs, g, a, kind, d1, d2, self.writer)
         if self.writer is not None:
             self.writer.flush()
+        check_fill_faults(out_dirs, self.device)
         return group44
 
     def forward(self, datas, output_dir, is_stereo=False, n_continuous=4):
@@ -577,6 +578,26 @@ class PreprocessPlusAugment(nn.Module):
             save_augment([output_dir], g, a, kind, d1, d2, self.writer)
         if self.writer is not None:
             self.writer.flush()
+        check_fill_faults([output_dir], self.device)
+
+
+def check_fill_faults(out_dirs: Optional[Sequence[str]], device) -> None:
+    """After a batch: raise if any hole-fill of it hit a bounded wait or bound
+    (ops.inpaint_faults; unreachable while the fill's invariants hold).  The
+    batch's files are removed first, so no wrong fill is left on disk and a
+    --skip-existing run redoes those images."""
+    if torch.device(device).type != "cuda":
+        return
+    from . import ops
+    bits = ops.inpaint_faults(reset=True)
+    if not bits:
+        return
+    for d in out_dirs or ():
+        for f in os.listdir(d) if os.path.isdir(d) else ():
+            if f.endswith(".npz"):
+                os.remove(os.path.join(d, f))
+    raise RuntimeError(f"hole-fill fault bits {bits:#x} (include/ofd_inpaint.h ofd_inpaint_faults): "
+                       f"the batch's fills are incomplete; its files were removed")
 
 
 # ---------------------------------------------------------------- npz writer

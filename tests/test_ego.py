@@ -5,11 +5,15 @@ geometry.BackprojectDepth / Project3D (geometry.py:17-67), and the first
 stage's ego-motion warps (preprocess.py:371-373, :385-387).
 
 Parity bar:
-* the flow plane (ops.ego_flow) equals the reference's own runs bit for bit
-  (tests/golden/pipeline.npz, ppa_fill_large.npz: since round 5 P = K @ T is
-  multiplied on the host in the reference's shapes);
-* against this repo's torch restatement evaluated on the GPU (torch's device
-  GEMMs round differently) the bar stays a tolerance -- |d flow| <= 8 ulp of
+* the parity bar: the flow plane (ops.ego_flow) equals the reference's own
+  CPU runs bit for bit (tests/golden/pipeline.npz, ppa_fill_large.npz: since
+  round 5 P = K @ T is multiplied on the host in the reference's shapes).
+  The reference pipeline itself runs on cuda:{gpu}; its device GEMM rounding
+  cannot be reproduced here (no CUDA device), so parity with that run is
+  unpinned;
+* a cross-check, not the parity bar: against this repo's torch restatement
+  evaluated on the GPU (torch's device GEMMs round differently) the flows
+  agree within a tolerance -- |d flow| <= 8 ulp of
   max(|p1|, size - 1) per axis (TOL_ULP below; p1 is computed in the
   normalised [-1, 1] domain and scaled by (size - 1) / 2, so its rounding
   error is set by the image size, not by |p1|: 9.5e-6 at 60x80, ~6e-5 at

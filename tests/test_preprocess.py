@@ -507,3 +507,24 @@ def test_augment_streams_give_the_same_batch_as_one_stream():
     for (ga, aa, ka, d1a, d2a), (gb, ab, kb, d1b, d2b) in zip(o0, o1):
         assert (ga, aa, ka) == (gb, ab, kb)
         assert torch.equal(d1a, d1b) and torch.equal(d2a, d2b), (ga, aa, ka)
+
+
+def test_fill_fault_discards_the_batch(tmp_path, monkeypatch):
+    """a fault bit of the hole-fill (a bounded wait that gave up)
+    must not leave a wrong fill on disk.  check_fill_faults, run after every
+    batch, removes the batch's npz files and raises; with no bit set it
+    keeps them.  (The fault word itself is stubbed: it cannot be provoked
+    while the fill's invariants hold.)"""
+    from opticalflowfromdepth_amd import ops, preprocess as pp
+    d = tmp_path / "img"
+    d.mkdir()
+    (d / "group.npz").write_bytes(b"x")
+    (d / "0_0_1.npz").write_bytes(b"x")
+    monkeypatch.setattr(ops, "inpaint_faults", lambda reset=True: 0)
+    pp.check_fill_faults([str(d)], "cuda:0")
+    assert sorted(os.listdir(d)) == ["0_0_1.npz", "group.npz"]
+    monkeypatch.setattr(ops, "inpaint_faults", lambda reset=True: 32)
+    with pytest.raises(RuntimeError, match="fault bits 0x20"):
+        pp.check_fill_faults([str(d)], "cuda:0")
+    assert os.listdir(d) == []
+    pp.check_fill_faults([str(d)], "cpu")  # host pipelines have no fault word
