@@ -134,6 +134,16 @@ int ofd_inpaint_seq_set_chipwide(int buckets, int min_pending);
  * Process-wide; returns the previous mode. */
 int ofd_inpaint_seq_set_colour(int mode);
 
+/* Workgroups per image of the sequential fill's levels-free colour pass
+ * (images of at least 2^18 pixels): 1 = one 1024-thread workgroup per image
+ * (one CU); k > 1 = k workgroups of 256 threads sharing the image's ready
+ * queue (k CUs: the colour pass is VALU-issue-bound on one).  Results are
+ * identical for every k.  force != 0 applies k to smaller images too (tests;
+ * k is lowered where an image has fewer than 4608 padded pixels per
+ * workgroup).  workgroups < 1 only queries; default OFD_SEQ_MW.  Returns the
+ * previous setting.  Process-wide. */
+int ofd_inpaint_seq_set_multi(int workgroups, int force);
+
 /* The device whose helper streams a grouped sequential fill on `stream`
  * would use: the stream's own device (helpers are kept per device and
  * created there on first use), or -1 if it cannot be told. */

@@ -66,6 +66,7 @@ SIGNATURES = {
     "ofd_inpaint_seq_set_pipeline": ([ctypes.c_int, ctypes.c_int, ctypes.c_int], ctypes.c_int),
     "ofd_inpaint_seq_set_chipwide": ([ctypes.c_int, ctypes.c_int], ctypes.c_int),
     "ofd_inpaint_seq_set_colour": ([ctypes.c_int], ctypes.c_int),
+    "ofd_inpaint_seq_set_multi": ([ctypes.c_int, ctypes.c_int], ctypes.c_int),
     "ofd_deflate_bound": ([_I64], _SZ),
     "ofd_deflate_workspace_bytes": ([_I64, _I64], _SZ),
     "ofd_deflate_batch": ([_P, _I64, _I64, _P, _P, _P, _P, _SZ, _P], ctypes.c_int),

@@ -2763,22 +2763,45 @@ __global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, int C, int H, 
 #ifndef OFD_DF_SLEEP  // ... and the wait's s_sleep between checks (64 clocks per unit)
 #define OFD_DF_SLEEP 1
 #endif
-constexpr int kDfCt = 2048;  // recent-colour table entries
 constexpr int kDfQ = 512;    // queue entries held in LDS (the rest in fr2)
+template <int kThr>
 struct C3DfLds {
-    float buf[kSlots3][kBufStride];
-    float res[kSlots3][9];
-    uint64_t ct[kDfCt];  // recent colours: (position + 1) | word << 32, by position mod kDfCt
+    static constexpr int kCt = kThr >= 1024 ? 2048 : 1024;  // recent-colour table entries
+    float buf[kThr / kL3][kBufStride];
+    float res[kThr / kL3][9];
+    uint64_t ct[kCt];  // recent colours: (position + 1) | word << 32, by position mod kCt
     uint64_t ring[kDfQ];  // queue entry y: (y + 1) | position << 32 at y mod kDfQ, or in fr2[y]
     uint32_t qh, qr, qp, inflight;
+    uint32_t gbase;       // kMW: the shared-queue slots the round-end flush reserved
 };
 constexpr int kPQh = 52, kPQt = 53;  // pipe words: the queue's head and tail
+// Several workgroups per image (kMW, ofd_inpaint_seq_set_multi): the image's
+// ready holes sit in RECORD's rq (claimed by a CAS on kPRqc), in the
+// workgroups' LDS queues, and in a shared queue in cy (a ring of en tagged
+// granules, (position << 32) | (slot + 1), head kPGh / tail kPGt, device-scope
+// atomics).  kPGo counts the holes queued in LDS or in the shared queue or
+// being coloured, so a workgroup with nothing left leaves only when every
+// workgroup of its image has nothing left either.
+constexpr int kPGh = 54, kPGt = 55, kPGo = 56;
+#ifndef OFD_MW_CAP  // kMW: LDS queue length past which a wave's new ready holes go to the shared queue
+#define OFD_MW_CAP 64
+#endif
+#ifndef OFD_MW_RELOAD  // kMW: a waiting hole re-reads a missing neighbour's word every this many tries
+#define OFD_MW_RELOAD 2
+#endif
 
-__global__ __launch_bounds__(1024) void sq_colour3df_kernel(SqWs w, int C, int H, int W, int e, int fin,
-                                                            uint64_t round_ticks) {
-    __shared__ C3DfLds L;
+template <int kThr, bool kMW>
+__global__ __launch_bounds__(kThr) void sq_colour3df_kernel(SqWs w, int C, int H, int W, int e, int fin,
+                                                            uint64_t round_ticks, int kw) {
+    __shared__ C3DfLds<kThr> L;
+    constexpr int kDfCt = C3DfLds<kThr>::kCt;
     const int tid = threadIdx.x, g = tid / kL3, gl = tid % kL3, lane = tid & 63;
-    const Img m = image(w, blockIdx.x);
+    // kMW: kw workgroups per image, image-major (blocks b * kw .. b * kw + kw - 1)
+    const int wr = kMW ? int(blockIdx.x) % kw : 0;
+    const Img m = image(w, kMW ? int(blockIdx.x) / kw : int(blockIdx.x));
+    // kMW: this workgroup's overflow slice of fr2 (LDS queue entries past kDfQ)
+    const uint32_t ovf = kMW ? uint32_t(m.en / kw) : 0u, ovf0 = uint32_t(wr) * ovf;
+    uint32_t *pw = m.pipe;
     const int eh = m.eh, ew = m.ew;
     const int wbias = 4 * ew + 4;
     (void)eh;
@@ -2807,16 +2830,20 @@ __global__ __launch_bounds__(1024) void sq_colour3df_kernel(SqWs w, int C, int H
 #else
 #define WOFF(k) ((WC(k) / 9 - 4) * ew + (WC(k) % 9 - 4))
 #endif
-    // the queue: carried entries, then RECORD's new ready holes
-    const uint32_t q0 = m.pipe[kPRqc], q1 = m.meta[2], h0 = m.pipe[kPQh], t0q = m.pipe[kPQt];
-    for (uint32_t x = tid; x < q1 - q0; x += 1024) m.fr2[t0q + x] = m.rq[q0 + x];
-    for (int x = tid; x < kDfCt; x += 1024) L.ct[x] = 0ull;
-    for (int x = tid; x < kDfQ; x += 1024) L.ring[x] = 0ull;
+    // the queue: carried entries, then RECORD's new ready holes (kMW: the
+    // LDS queue starts empty; rq and the shared queue are claimed directly)
+    const uint32_t q0 = m.pipe[kPRqc], q1 = m.meta[2], h0 = kMW ? 0u : m.pipe[kPQh], t0q = kMW ? 0u : m.pipe[kPQt];
+    if constexpr (!kMW)
+        for (uint32_t x = tid; x < q1 - q0; x += kThr) m.fr2[t0q + x] = m.rq[q0 + x];
+    for (int x = tid; x < kDfCt; x += kThr) L.ct[x] = 0ull;
+    for (int x = tid; x < kDfQ; x += kThr) L.ring[x] = 0ull;
     if (tid == 0) {
         L.qh = h0;
-        L.qr = L.qp = t0q + (q1 - q0);
+        L.qr = L.qp = kMW ? 0u : t0q + (q1 - q0);
         L.inflight = 0u;
-        if (h0 < t0q + (q1 - q0)) {
+        const bool work = kMW ? (q0 < q1 || __hip_atomic_load(pw + kPGo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)
+                              : h0 < t0q + (q1 - q0);
+        if (work && wr == 0) {
             if (m.pipe[kPCRounds] == 0u) put64(m.pipe + kPTc0, wall_clock64());
             m.pipe[kPCRounds] += 1u;
         }
@@ -2867,6 +2894,58 @@ __global__ __launch_bounds__(1024) void sq_colour3df_kernel(SqWs w, int C, int H
                 break;
             }
         }
+        // kMW, nothing in the LDS queue: claim up to 8 holes of RECORD's rq,
+        // else of the shared queue (src 1 / 2; 0 = the LDS queue)
+        uint32_t src = 0;
+        if constexpr (kMW) {
+            if (take == 0u) {
+                uint32_t tk = 0, qb = 0, sr = 0;
+                if (lane == 0) {
+                    atomicAdd(&L.inflight, 8u);  // before the claim: no false "all done"
+                    uint32_t c = __hip_atomic_load(pw + kPRqc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    // rq's holes are counted when claimed: 8 provisionally,
+                    // returned before the claim, so no workgroup of the image
+                    // sees rq drained and the count at 0 while this batch runs
+                    const bool try_rq = c < q1;
+                    if (try_rq) {
+                        (void)__hip_atomic_fetch_add(pw + kPGo, 8u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    }
+                    for (int t = 0; t < 64 && c < q1 && tk == 0u; ++t) {
+                        const uint32_t want = q1 - c < 8u ? q1 - c : 8u;
+                        const uint32_t o = atomicCAS(pw + kPRqc, c, c + want);
+                        if (o == c) {
+                            tk = want;
+                            qb = c;
+                            sr = 1u;
+                        } else {
+                            c = o;
+                        }
+                    }
+                    if (try_rq && tk < 8u)
+                        (void)__hip_atomic_fetch_sub(pw + kPGo, 8u - tk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (tk == 0u) {
+                        uint32_t gh = __hip_atomic_load(pw + kPGh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        const uint32_t gt = __hip_atomic_load(pw + kPGt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        for (int t = 0; t < 64 && gh < gt && tk == 0u; ++t) {
+                            const uint32_t want = gt - gh < 8u ? gt - gh : 8u;
+                            const uint32_t o = atomicCAS(pw + kPGh, gh, gh + want);
+                            if (o == gh) {
+                                tk = want;
+                                qb = gh;
+                                sr = 2u;
+                            } else {
+                                gh = o;
+                            }
+                        }
+                    }
+                    atomicSub(&L.inflight, 8u - tk);
+                }
+                take = __shfl(tk, 0);
+                qbase = __shfl(qb, 0);
+                src = __shfl(sr, 0);
+            }
+        }
         if (take == 0u) {
             uint32_t quit = 0;
             if (lane == 0) {
@@ -2874,14 +2953,18 @@ __global__ __launch_bounds__(1024) void sq_colour3df_kernel(SqWs w, int C, int H
                 const uint32_t h = __hip_atomic_load(&L.qh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 const uint32_t pq = __hip_atomic_load(&L.qp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 const uint32_t inf = __hip_atomic_load(&L.inflight, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                quit = (h >= pq && inf == 0u) || now >= deadline ? 1u : 0u;
+                bool none = h >= pq && inf == 0u;
+                if (kMW && none)  // the image's other workgroups may still queue holes for the shared queue
+                    none = __hip_atomic_load(pw + kPRqc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= q1 &&
+                           __hip_atomic_load(pw + kPGo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
+                quit = none || now >= deadline ? 1u : 0u;
                 if (now - tstart > 400000000ull) {  // 4 s: cannot happen
                     atomicOr(&g_sq_fault, 32u);
                     quit = 1u;
                 }
             }
             if (__shfl(quit, 0)) break;
-            __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_s_sleep(kMW ? 2 : 1);
             continue;
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -2894,7 +2977,28 @@ __global__ __launch_bounds__(1024) void sq_colour3df_kernel(SqWs w, int C, int H
             const bool act = uint32_t(g & 7) < take;  // the wave's 8 hole slots
             const uint32_t y = qbase + uint32_t(g & 7);
             uint64_t ent = __shfl(se, g & 7);
-            if (act && uint32_t(ent) != y + 1u) ent = m.fr2[y];  // not in the ring: fr2 (pixel << 32 | pixel)
+            if constexpr (kMW) {
+                if (src == 1u) {
+                    ent = act ? m.rq[y] : 0ull;  // RECORD's (pixel << 32 | pixel), written before this launch
+                } else if (src == 2u) {
+                    if (act) {  // the shared queue's granule: poll until its tag is the slot's
+                        const uint32_t sl = y % uint32_t(m.en);
+                        for (int t = 0;; ++t) {
+                            ent = __hip_atomic_load(m.cy + sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            if (uint32_t(ent) == y + 1u) break;
+                            if (t > (1 << 22)) {  // cannot happen: a reserved slot is written right after
+                                atomicOr(&g_sq_fault, 32u);
+                                break;
+                            }
+                            __builtin_amdgcn_s_sleep(1);
+                        }
+                    }
+                } else if (act && uint32_t(ent) != y + 1u) {
+                    ent = m.fr2[ovf0 + y % ovf];  // not in the ring: this workgroup's overflow slice
+                }
+            } else if (act && uint32_t(ent) != y + 1u) {
+                ent = m.fr2[y];  // not in the ring: fr2 (pixel << 32 | pixel)
+            }
             const uint32_t p = uint32_t(ent >> 32), idx = p;
             const int i = int(p / uint32_t(ew)), j = int(p - uint32_t(i) * uint32_t(ew));
             // the level's one round of loads
@@ -2944,7 +3048,9 @@ __global__ __launch_bounds__(1024) void sq_colour3df_kernel(SqWs w, int C, int H
                         if (gl == 0) atomicOr(&g_sq_fault, 32u);
                         break;
                     }
-                    const bool reload = (tries & 7) == 7;  // the table entry may have been displaced
+                    // the table entry may have been displaced, or (kMW) the
+                    // neighbour coloured by another workgroup of the image
+                    const bool reload = kMW ? (tries % OFD_MW_RELOAD) == OFD_MW_RELOAD - 1 : (tries & 7) == 7;
 #pragma unroll
                     for (int k = 0; k < 8; ++k) asm volatile("" : "+v"(tb[k]));  // no hoisted offsets (spills)
 #pragma unroll
@@ -3052,15 +3158,38 @@ __global__ __launch_bounds__(1024) void sq_colour3df_kernel(SqWs w, int C, int H
                 }
                 const uint32_t tot = __shfl(incl, 63);
                 if (tot == 0u) return;  // wave-uniform
-                uint32_t rb = 0, hq = 0;
+                uint32_t rb = 0, hq = 0, sp = 0;
                 if (lane == 63) {
-                    rb = atomicAdd(&L.qr, tot);
                     hq = __hip_atomic_load(&L.qh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if constexpr (kMW) {
+                        // counted before any of them can be taken (the add has
+                        // returned before the slots are published), so the
+                        // image's count never misses a queued hole
+                        const uint32_t len = __hip_atomic_load(&L.qr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) - hq;
+                        sp = len + tot > uint32_t(OFD_MW_CAP) ? 1u : 0u;
+                        (void)__hip_atomic_fetch_add(pw + kPGo, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        rb = sp ? atomicAdd(pw + kPGt, tot) : atomicAdd(&L.qr, tot);
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    } else {
+                        rb = atomicAdd(&L.qr, tot);
+                    }
                 }
                 rb = __shfl(rb, 63);
                 hq = __shfl(hq, 63);
+                sp = __shfl(sp, 63);
                 uint32_t f = rb + incl - cnt;
                 bool glob = false;
+                if (kMW && sp) {  // to the shared queue: tagged granules, no ordered publish
+#pragma unroll
+                    for (int k = 0; k < 8; ++k)
+                        if (rmask & (1u << k)) {
+                            const auto q = IX32(p + uint32_t(WOFF(k)));
+                            __hip_atomic_store(m.cy + f % uint32_t(m.en), (uint64_t(q) << 32) | uint64_t(f + 1u),
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            ++f;
+                        }
+                    return;
+                }
 #pragma unroll
                 for (int k = 0; k < 8; ++k)
                     if (rmask & (1u << k)) {
@@ -3069,7 +3198,7 @@ __global__ __launch_bounds__(1024) void sq_colour3df_kernel(SqWs w, int C, int H
                             __hip_atomic_store(&L.ring[f & uint32_t(kDfQ - 1)], (uint64_t(q) << 32) | uint64_t(f + 1u),
                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         } else {
-                            m.fr2[f] = (uint64_t(q) << 32) | uint64_t(q);
+                            m.fr2[kMW ? ovf0 + f % ovf : f] = (uint64_t(q) << 32) | uint64_t(q);
                             glob = true;
                         }
                         ++f;
@@ -3195,7 +3324,11 @@ __global__ __launch_bounds__(1024) void sq_colour3df_kernel(SqWs w, int C, int H
                 const unsigned u1 = __shfl(u, hl0 + 1), u2 = __shfl(u, hl0 + 2);
                 if (act && gl == 0) {
                     const uint32_t word = u | (u1 << 8) | (u2 << 16) | 0xFF000000u;
-                    m.shd[int64_t(i - 1) * W + (j - 1)] = word;
+                    if constexpr (kMW)  // write-through (sc1): the other workgroups' sc1 polls see it
+                        __hip_atomic_store(m.shd + (int64_t(i - 1) * W + (j - 1)), word, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                    else
+                        m.shd[int64_t(i - 1) * W + (j - 1)] = word;
                     __hip_atomic_store(&L.ct[p & uint32_t(kDfCt - 1)], (uint64_t(word) << 32) | uint64_t(p + 1u),
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
@@ -3212,14 +3345,38 @@ __global__ __launch_bounds__(1024) void sq_colour3df_kernel(SqWs w, int C, int H
             SQ_ACC(1, ca, c3);  // the append
             SQ_ACC(5, c3, c4);
         }
-        if (lane == 0) atomicSub(&L.inflight, take);
+        if (lane == 0) {
+            // kMW: the image's count drops by this batch's holes, after the
+            // batch's own additions have returned (append_ready waits for them)
+            if (kMW) (void)__hip_atomic_fetch_sub(pw + kPGo, take, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            atomicSub(&L.inflight, take);
+        }
         ++batches;
         if (__shfl(lane == 0 ? (wall_clock64() >= deadline ? 1u : 0u) : 0u, 0)) break;  // the rest is carried
     }
     if (lane == 0) atomicAdd(&m.meta[6], batches);
     __syncthreads();
+    if constexpr (kMW) {
+        // the unclaimed entries of the LDS queue go to the shared queue for the
+        // next round (still counted in kPGo)
+        const uint32_t hq = L.qh, pq = L.qp;
+        if (tid == 0 && pq > hq) L.gbase = atomicAdd(pw + kPGt, pq - hq);
+        __syncthreads();
+        const uint32_t gb = L.gbase;
+        for (uint32_t y = hq + uint32_t(tid); y < pq; y += kThr) {
+            const uint64_t v = L.ring[y & uint32_t(kDfQ - 1)];
+            const uint32_t q = uint32_t(uint32_t(v) == y + 1u ? (v >> 32) : (m.fr2[ovf0 + y % ovf] >> 32));
+            const uint32_t sl = gb + (y - hq);
+            __hip_atomic_store(m.cy + sl % uint32_t(m.en), (uint64_t(q) << 32) | uint64_t(sl + 1u), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (tid == 0 && wr == 0 && pq <= hq &&
+            __hip_atomic_load(pw + kPGo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+            put64(m.pipe + kPTc1, wall_clock64());
+        return;
+    }
     // the unclaimed entries still in the ring go to fr2 for the next round
-    for (uint32_t y = L.qh + uint32_t(tid); y < L.qp; y += 1024) {
+    for (uint32_t y = L.qh + uint32_t(tid); y < L.qp; y += kThr) {
         const uint64_t v = L.ring[y & uint32_t(kDfQ - 1)];
         if (uint32_t(v) == y + 1u) m.fr2[y] = (v & 0xFFFFFFFF00000000ull) | (v >> 32);
     }
@@ -3396,6 +3553,19 @@ int g_df_colour = [] {
     const char *e = getenv("OFD_SEQ_DF");
     return e ? (atoi(e) != 0 ? 1 : 0) : 1;
 }();  // ofd_inpaint_seq_set_chipwide (tests: 0 keeps small marches chip-wide)
+// Workgroups per image of the levels-free colour pass (kMW: 256 threads
+// each, sharing the image's queues; 1 = one 1024-thread workgroup, the
+// single-CU pass).  ofd_inpaint_seq_set_multi, default OFD_SEQ_MW (else
+// OFD_SEQ_MW_DEFAULT); images below kPipeMinPixels always take one.
+#ifndef OFD_SEQ_MW_DEFAULT
+#define OFD_SEQ_MW_DEFAULT 1
+#endif
+int g_seq_multi = [] {
+    const char *e = getenv("OFD_SEQ_MW");
+    const int v = e ? atoi(e) : OFD_SEQ_MW_DEFAULT;
+    return v < 1 ? 1 : (v > 16 ? 16 : v);
+}();
+int g_mw_force = 0;  // ofd_inpaint_seq_set_multi(k, 1): also below kPipeMinPixels (tests)
 int cw_buckets_setting() {
     if (g_cw_buckets < 0) {
         const char *e = getenv("OFD_SEQ_CW");
@@ -3453,6 +3623,15 @@ int ofd_inpaint_seq_helper_device(void *stream) {
 int ofd_inpaint_seq_set_colour(int mode) {
     const int prev = g_df_colour;
     if (mode >= 0) g_df_colour = mode != 0 ? 1 : 0;
+    return prev;
+}
+
+int ofd_inpaint_seq_set_multi(int workgroups, int force) {
+    const int prev = g_seq_multi;
+    if (workgroups >= 1) {
+        g_seq_multi = workgroups > 16 ? 16 : workgroups;
+        g_mw_force = force ? 1 : 0;
+    }
     return prev;
 }
 
@@ -3530,6 +3709,10 @@ int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float 
     }
     const int cwk = cw_buckets_setting();
     const bool df_colour = g_df_colour != 0;
+    // kMW: each workgroup's overflow slice of fr2 (en / mw entries) must hold
+    // its LDS queue's worst case: kDfQ + OFD_MW_CAP + 4 waves x 480 new holes
+    int mw = (df_colour && rec3 && (H * W >= kPipeMinPixels || g_mw_force)) ? g_seq_multi : 1;
+    while (mw > 1 && en / mw < 4608) --mw;
 
     // one chunk of nb images (workspace w) on stream s
     auto run_chunk = [&](const SqWs &w, int64_t b0, int64_t nb, hipStream_t s) {
@@ -3570,12 +3753,18 @@ int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float 
                 hipLaunchKernelGGL(sq_cw_end_kernel, dim3(unsigned(segs)), dim3(64), 0, s, w, k);
             }
         }
+        // kMW: the shared queues' granules are tagged by slot, which restarts
+        // at 0 every fill -- clear the previous fill's tags
+        if (rec3 && mw > 1) (void)hipMemsetAsync(w.cy, 0, size_t(nb) * size_t(w.en) * 8, s);
         auto round = [&](hipStream_t rs, int e, int fin) {  // one RECORD / COLOUR3 round
             hipLaunchKernelGGL(sq_pace_kernel, dim3(1), dim3(256), 0, rs, w, int(nb), e, fin, pipe_ticks, 4 * pipe_ticks);
             hipLaunchKernelGGL(sq_record3_kernel, rgrid, dim3(256), 0, rs, w);
-            if (df_colour)
-                hipLaunchKernelGGL(sq_colour3df_kernel, dim3(unsigned(nb)), dim3(1024), 0, rs, w, int(C), int(H), int(W),
-                                   e, fin, pipe_ticks);
+            if (df_colour && mw > 1)
+                hipLaunchKernelGGL((sq_colour3df_kernel<256, true>), dim3(unsigned(nb * mw)), dim3(256), 0, rs, w, int(C),
+                                   int(H), int(W), e, fin, pipe_ticks, mw);
+            else if (df_colour)
+                hipLaunchKernelGGL((sq_colour3df_kernel<1024, false>), dim3(unsigned(nb)), dim3(1024), 0, rs, w, int(C),
+                                   int(H), int(W), e, fin, pipe_ticks, 1);
             else
                 hipLaunchKernelGGL(sq_colour3_kernel, dim3(unsigned(nb)), dim3(1024), 0, rs, w, int(C), int(H), int(W), e,
                                    fin, pipe_ticks);

@@ -698,3 +698,60 @@ def test_inpaint_sequential_pipeline_settings_agree_on_warped_images(rounds, us,
     assert np.array_equal(got, exp)
     from opticalflowfromdepth_amd import _native
     assert _native.lib().ofd_inpaint_faults(1) == 0
+
+
+# ------------------------------------------------------------------ several workgroups per image
+@pytest.fixture
+def seq_multi():
+    """Sets the levels-free colour pass's workgroups per image for one test
+    (ofd_inpaint_seq_set_multi) and restores the setting afterwards."""
+    from opticalflowfromdepth_amd import _native
+    lib = _native.lib()
+    prev = lib.ofd_inpaint_seq_set_multi(0, 0)
+    yield lambda k, force=0: lib.ofd_inpaint_seq_set_multi(k, force)
+    lib.ofd_inpaint_seq_set_multi(prev, 0)
+
+
+def _warped_rgb(seeds, h, w):
+    from opticalflowfromdepth_amd import forward_warp_flow, synth
+    dev = torch.device("cuda:0")
+    obj, flow, depth = synth.stage_one_batch(seeds, h, w, dev)
+    out, valid, coll = forward_warp_flow(obj, flow, depth)
+    return (out[:, 0:3] * valid).contiguous(), valid, coll
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [1, 2, 4, 8])
+def test_inpaint_sequential_multi_workgroup_on_warped_images(k, seq_multi):
+    """The levels-free colour pass with k workgroups per image (the image's
+    ready holes shared through RECORD's queue, each workgroup's LDS queue and
+    a shared queue of tagged granules; colours handed across CUs by
+    write-through stores): warped 768x1024 images, 8 at once, pipelined as by
+    default -- the oracle's cv2 order bit for bit, no fault bit."""
+    from opticalflowfromdepth_amd import _native, ops
+    rgb, valid, coll = _warped_rgb([12345, 12346, 12377, 12378, 12401, 12402, 12433, 12434], 768, 1024)
+    seq_multi(k)
+    got = ops.inpaint(rgb, valid, coll, order="sequential").cpu().numpy()
+    exp = oracle.inpaint(rgb.cpu().numpy(), valid.cpu().numpy(), coll.cpu().numpy(), 3, layered=False)
+    assert np.array_equal(got, exp), f"k={k}: {int((got != exp).sum())} values differ"
+    assert _native.lib().ofd_inpaint_faults(1) == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rounds,us", [(0, 2000), (48, 100), (64, 2)])
+@pytest.mark.parametrize("shape", [(192, 256), (384, 512)])
+def test_inpaint_sequential_multi_workgroup_rounds_and_shapes(shape, rounds, us, seq_multi, seq_pipeline):
+    """k = 4 forced onto smaller warped images (fewer padded pixels per
+    workgroup; each workgroup's overflow slice is smaller), with no rounds
+    beside the marches, many short ones and very short ones (every round
+    flushes its LDS queues into the shared queue for the next): bit for bit
+    the oracle's cv2 order."""
+    from opticalflowfromdepth_amd import _native, ops
+    h, w = shape
+    rgb, valid, coll = _warped_rgb([12345, 12346, 12377, 12378], h, w)
+    seq_multi(4, 1)
+    seq_pipeline(rounds, us, 1)
+    got = ops.inpaint(rgb, valid, coll, order="sequential").cpu().numpy()
+    exp = oracle.inpaint(rgb.cpu().numpy(), valid.cpu().numpy(), coll.cpu().numpy(), 3, layered=False)
+    assert np.array_equal(got, exp), f"{shape} rounds {rounds}: {int((got != exp).sum())} values differ"
+    assert _native.lib().ofd_inpaint_faults(1) == 0
