@@ -136,9 +136,10 @@ int ofd_inpaint_seq_set_colour(int mode);
 
 /* Workgroups per image of the sequential fill's levels-free colour pass
  * (images of at least 2^18 pixels): 1 = one 1024-thread workgroup per image
- * (one CU); k > 1 = k workgroups of 256 threads sharing the image's ready
+ * (one CU); k > 1 = k workgroups of 512 threads sharing the image's ready
  * queue (k CUs: the colour pass is VALU-issue-bound on one).  Results are
- * identical for every k.  force != 0 applies k to smaller images too (tests;
+ * identical for every k (default 4: 37.6 -> 35.5 ms per 64 warped 768x1024
+ * images).  force != 0 applies k to smaller images too (tests;
  * k is lowered where an image has fewer than 4608 padded pixels per
  * workgroup).  workgroups < 1 only queries; default OFD_SEQ_MW.  Returns the
  * previous setting.  Process-wide. */

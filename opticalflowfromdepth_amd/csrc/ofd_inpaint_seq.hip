@@ -2270,6 +2270,7 @@ constexpr int kFrCap = 1280;             // LDS frontier entries per buffer
 constexpr int kBufStride = (kTerm3 + 55) / 64 * 64 + 8;
 static_assert(kBufStride >= kTerm3 && kBufStride % 64 == 8, "slot stride");
 
+
 // e-th position (raster order) of the window including its centre
 __device__ __forceinline__ void val_pos(int e, int &a, int &b) {
     int n = 0;
@@ -2784,8 +2785,12 @@ constexpr int kPQh = 52, kPQt = 53;  // pipe words: the queue's head and tail
 // workgroup of its image has nothing left either.
 constexpr int kPGh = 54, kPGt = 55, kPGo = 56;
 #ifndef OFD_MW_CAP  // kMW: LDS queue length past which a wave's new ready holes go to the shared queue
-#define OFD_MW_CAP 64
+#define OFD_MW_CAP 16
 #endif
+#ifndef OFD_MW_THR  // kMW: threads per workgroup
+#define OFD_MW_THR 512
+#endif
+static_assert(OFD_MW_THR <= 512, "kMW overflow slices are sized for at most 8 waves per workgroup");
 #ifndef OFD_MW_RELOAD  // kMW: a waiting hole re-reads a missing neighbour's word every this many tries
 #define OFD_MW_RELOAD 2
 #endif
@@ -2901,7 +2906,10 @@ __global__ __launch_bounds__(kThr) void sq_colour3df_kernel(SqWs w, int C, int H
             if (take == 0u) {
                 uint32_t tk = 0, qb = 0, sr = 0;
                 if (lane == 0) {
-                    atomicAdd(&L.inflight, 8u);  // before the claim: no false "all done"
+                    // no provisional L.inflight here: the image's count kPGo
+                    // covers a claimed batch until its end (idle waves adding
+                    // to L.inflight while they poll kept their workgroup from
+                    // ever seeing itself idle)
                     uint32_t c = __hip_atomic_load(pw + kPRqc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     // rq's holes are counted when claimed: 8 provisionally,
                     // returned before the claim, so no workgroup of the image
@@ -2939,7 +2947,7 @@ __global__ __launch_bounds__(kThr) void sq_colour3df_kernel(SqWs w, int C, int H
                             }
                         }
                     }
-                    atomicSub(&L.inflight, 8u - tk);
+                    if (tk) atomicAdd(&L.inflight, tk);  // the batch end's subtraction is uniform
                 }
                 take = __shfl(tk, 0);
                 qbase = __shfl(qb, 0);
@@ -2960,6 +2968,15 @@ __global__ __launch_bounds__(kThr) void sq_colour3df_kernel(SqWs w, int C, int H
                 quit = none || now >= deadline ? 1u : 0u;
                 if (now - tstart > 400000000ull) {  // 4 s: cannot happen
                     atomicOr(&g_sq_fault, 32u);
+#ifdef OFD_MW_DEBUG
+                    if (kMW)
+                        printf("MWDBG idle img %d wr %d fin %d h %u pq %u inf %u rqc %u q1 %u go %u gh %u gt %u\n",
+                               int(blockIdx.x) / kw, wr, fin, h, pq, inf,
+                               __hip_atomic_load(pw + kPRqc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), q1,
+                               __hip_atomic_load(pw + kPGo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                               __hip_atomic_load(pw + kPGh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                               __hip_atomic_load(pw + kPGt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+#endif
                     quit = 1u;
                 }
             }
@@ -2988,6 +3005,9 @@ __global__ __launch_bounds__(kThr) void sq_colour3df_kernel(SqWs w, int C, int H
                             if (uint32_t(ent) == y + 1u) break;
                             if (t > (1 << 22)) {  // cannot happen: a reserved slot is written right after
                                 atomicOr(&g_sq_fault, 32u);
+#ifdef OFD_MW_DEBUG
+                                if (gl == 0) printf("MWDBG gqpoll wr %d y %u tag %u\n", wr, y, uint32_t(ent));
+#endif
                                 break;
                             }
                             __builtin_amdgcn_s_sleep(1);
@@ -3046,6 +3066,9 @@ __global__ __launch_bounds__(kThr) void sq_colour3df_kernel(SqWs w, int C, int H
                 for (int tries = 0; __any(pend != 0u); ++tries) {
                     if (tries > (1 << 20)) {  // cannot happen: every released hole is being coloured
                         if (gl == 0) atomicOr(&g_sq_fault, 32u);
+#ifdef OFD_MW_DEBUG
+                        if (gl == 0) printf("MWDBG flagwait wr %d p %u pend %x\n", wr, p, pend);
+#endif
                         break;
                     }
                     // the table entry may have been displaced, or (kMW) the
@@ -3211,6 +3234,9 @@ __global__ __launch_bounds__(kThr) void sq_colour3df_kernel(SqWs w, int C, int H
                     for (int t = 0; __hip_atomic_load(&L.qp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != rb; ++t) {
                         if (t > (1 << 22)) {  // cannot happen: earlier reservations publish without waiting
                             atomicOr(&g_sq_fault, 32u);
+#ifdef OFD_MW_DEBUG
+                            printf("MWDBG publish wr %d rb %u qp %u\n", wr, rb, L.qp);
+#endif
                             break;
                         }
                         __builtin_amdgcn_s_sleep(1);
@@ -3558,7 +3584,7 @@ int g_df_colour = [] {
 // single-CU pass).  ofd_inpaint_seq_set_multi, default OFD_SEQ_MW (else
 // OFD_SEQ_MW_DEFAULT); images below kPipeMinPixels always take one.
 #ifndef OFD_SEQ_MW_DEFAULT
-#define OFD_SEQ_MW_DEFAULT 1
+#define OFD_SEQ_MW_DEFAULT 4
 #endif
 int g_seq_multi = [] {
     const char *e = getenv("OFD_SEQ_MW");
@@ -3710,7 +3736,7 @@ int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float 
     const int cwk = cw_buckets_setting();
     const bool df_colour = g_df_colour != 0;
     // kMW: each workgroup's overflow slice of fr2 (en / mw entries) must hold
-    // its LDS queue's worst case: kDfQ + OFD_MW_CAP + 4 waves x 480 new holes
+    // its LDS queue's worst case: kDfQ + OFD_MW_CAP + 8 waves x 480 new holes
     int mw = (df_colour && rec3 && (H * W >= kPipeMinPixels || g_mw_force)) ? g_seq_multi : 1;
     while (mw > 1 && en / mw < 4608) --mw;
 
@@ -3760,7 +3786,7 @@ int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float 
             hipLaunchKernelGGL(sq_pace_kernel, dim3(1), dim3(256), 0, rs, w, int(nb), e, fin, pipe_ticks, 4 * pipe_ticks);
             hipLaunchKernelGGL(sq_record3_kernel, rgrid, dim3(256), 0, rs, w);
             if (df_colour && mw > 1)
-                hipLaunchKernelGGL((sq_colour3df_kernel<256, true>), dim3(unsigned(nb * mw)), dim3(256), 0, rs, w, int(C),
+                hipLaunchKernelGGL((sq_colour3df_kernel<OFD_MW_THR, true>), dim3(unsigned(nb * mw)), dim3(OFD_MW_THR), 0, rs, w, int(C),
                                    int(H), int(W), e, fin, pipe_ticks, mw);
             else if (df_colour)
                 hipLaunchKernelGGL((sq_colour3df_kernel<1024, false>), dim3(unsigned(nb)), dim3(1024), 0, rs, w, int(C),
