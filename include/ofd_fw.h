@@ -122,6 +122,15 @@ int ofd_fw_set_persist_min(int tiles_per_slot);
  * against concurrent calls. */
 int ofd_fw_set_pack(int on);
 
+/* Short calls of the fused TILE engine (fewer tiles than persist_min() per
+ * resident SPLAT slot: one SPLAT workgroup per tile) on plain coordinate
+ * sources (FW on a flow or on safe coordinates, the bf16 warp) use 128 x 16
+ * target tiles instead of 128 x 32: twice the workgroups, a shorter drain.
+ * on = 1 (default) / 0 for subsequent calls (also OFD_FW_SHORT_TILES=0); any
+ * other value only queries.  Results are identical.  Returns the previous
+ * setting.  Process-wide, not thread-safe against concurrent calls. */
+int ofd_fw_set_short_tiles(int on);
+
 /* Benchmark hook: when non-NULL, the given hipEvent_t's are recorded on the
  * launch stream right before the first and right after the last launch of
  * each subsequent f32 call's dominant kernel: SPLAT (TILE engine), RESOLVE

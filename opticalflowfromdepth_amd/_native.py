@@ -38,6 +38,7 @@ SIGNATURES = {
     "ofd_fw_set_pack": ([ctypes.c_int], ctypes.c_int),
     "ofd_fw_set_profile_events": ([_P, _P], ctypes.c_int),
     "ofd_fw_set_profile_bin_event": ([_P], ctypes.c_int),
+    "ofd_fw_set_short_tiles": ([ctypes.c_int], ctypes.c_int),
     "ofd_fw_workspace_bytes": ([_I64, _I64, _I64, ctypes.c_int], _SZ),
     "ofd_fw_workspace_init": ([_P, _SZ, _P], ctypes.c_int),
     "ofd_fw_forward_warping_f32": ([_P] * 7 + [_I64] * 4 + [_P, _SZ, _P], ctypes.c_int),

@@ -628,10 +628,11 @@ struct TileGeom {
     int nsegx, nseg;             // segments (SEGB blocks of one block row) per image
 };
 
-inline TileGeom make_geom(int64_t H, int64_t W) {
+// th: the tile height (TH, or kShortTH for short calls: run_f32)
+inline TileGeom make_geom(int64_t H, int64_t W, int th = TH) {
     TileGeom g;
     g.tilesX = int((W + TW - 1) / TW);
-    g.tilesY = int((H + TH - 1) / TH);
+    g.tilesY = int((H + th - 1) / th);
     g.ntiles = g.tilesX * g.tilesY;
     g.nsbx = int((W + SBW - 1) / SBW);
     g.nsby = int((H + SBH - 1) / SBH);
@@ -647,8 +648,12 @@ inline size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 // (HW u32), per-tile spill flags, and the target-tile boxes of every source
 // segment and block; plus, once per chunk slab, the persistent SPLAT's tile
 // queue words (inside the per-image slack).
+// Sized (and carved) for the shorter tiles, which have the most tiles: one
+// layout serves both tile heights, so a call may pick either.
+constexpr int kShortTH = 16;  // tile height of short calls (run_f32)
+static_assert(kShortTH <= TH && TH % kShortTH == 0, "short tiles");
 inline size_t per_image_bytes(int64_t H, int64_t W) {
-    const TileGeom g = make_geom(H, W);
+    const TileGeom g = make_geom(H, W, kShortTH);
     return size_t(H) * size_t(W) * 12 + size_t(g.ntiles) * 4 + size_t(g.nseg) * 8 + size_t(g.nsb) * 8 + 256;
 }
 
@@ -714,8 +719,9 @@ constexpr int kListCap = 1024;  // candidate blocks examined per batch
 constexpr int kResolveWX = 2, kResolveRows = 8;  // RESOLVE workgroup = 128 x 8 targets
 constexpr unsigned int WIN_NONE = 0xFFFFFFFFu;
 
-struct TileLds {
-    unsigned long long zk[TW * TH];
+template <int kTH>
+struct TileLdsT {
+    unsigned long long zk[TW * kTH];
     unsigned int seg[kSegCap];
     unsigned int blk[kListCap];
     unsigned int nseg, nblk, flag;
@@ -759,16 +765,18 @@ __device__ __forceinline__ unsigned quad_min_pk16(unsigned v) {
 static_assert(TW * TH <= 4096 && MAX_TILES_PER_BLOCK <= 15, "packed target: 12-bit tile offset, 4-bit tile index");
 constexpr unsigned short CODE_NONE = 0xFFFF;
 
+template <int TH>
 __device__ __forceinline__ unsigned short pack_target(int tx, int ty, int t0x, int t0y, int bw) {
     if (tx < 0) return CODE_NONE;
     const int k = (ty / TH - t0y) * bw + (tx / TW - t0x);
     return (unsigned short)((unsigned(k) << 12) | unsigned((ty % TH) * TW + tx % TW));
 }
 
-template <typename Coords, bool kPack = false, bool kVec = false>
+template <typename Coords, bool kPack = false, bool kVec = false, int kTH = TH>
 __device__ __forceinline__ void bin_segment(const Coords &co, const float *__restrict__ depth, const ChunkArgs &a,
                                                int H, int W, int64_t HW, const TileGeom &g, int64_t sgg,
                                                const typename Coords::V (&x)[2][4], const typename Coords::V (&y)[2][4]) {
+    constexpr int TH = kTH;  // this call's tile height (shadows the default)
     const Ws &ws = a.ws;
     const int lane = lane_id();
     const int bl = int(sgg / g.nseg);
@@ -826,7 +834,7 @@ __device__ __forceinline__ void bin_segment(const Coords &co, const float *__res
             for (int e = 0; e < 4; ++e) {
                 int tx = -1, ty = -1;
                 if (boxed && i0 + e < W) co.target(b, i0 + e, j, x[q][e], y[q][e], H, W, tx, ty);
-                c[e] = pack_target(tx, ty, t0x, t0y, bw);
+                c[e] = pack_target<TH>(tx, ty, t0x, t0y, bw);
             }
             const int64_t p = int64_t(j) * W + i0;
             if constexpr (kVec) {
@@ -882,7 +890,7 @@ struct BinMinW<EgoCoords<D>> {
     static constexpr int value = 1;
 };
 
-template <typename Coords, bool kVec, int kSPW = 1, bool kPack = false>
+template <typename Coords, bool kVec, int kSPW = 1, bool kPack = false, int kTH = TH>
 __global__ __launch_bounds__(kWarpThreads, BinMinW<Coords>::value) void bin_kernel(Coords co, const float *__restrict__ depth, ChunkArgs a,
                                                               int H, int W, int64_t HW, TileGeom g) {
     using V = typename Coords::V;
@@ -907,7 +915,7 @@ __global__ __launch_bounds__(kWarpThreads, BinMinW<Coords>::value) void bin_kern
     }
 #pragma unroll
     for (int s = 0; s < kSPW; ++s)
-        if (sg0 + s < nsg) bin_segment<Coords, kPack, kVec>(co, depth, a, H, W, HW, g, sg0 + s, x[s], y[s]);  // wave-uniform
+        if (sg0 + s < nsg) bin_segment<Coords, kPack, kVec, kTH>(co, depth, a, H, W, HW, g, sg0 + s, x[s], y[s]);  // wave-uniform
 }
 
 // ---- SPLAT.  Workgroup id -> XCD-aware tile: dispatch is round-robin over the
@@ -987,10 +995,10 @@ struct SplatIO {
 // SPLAT launch shape: threads per workgroup, gather targets in flight per
 // thread (fused publish), minimum waves per SIMD (__launch_bounds__), 4-block
 // slots in flight per wave, publish store policy, tile order (probe knobs).
-template <int kThr_, int kGT_, int kMinW_, int kUF_ = kSplatU, int kNTPub_ = 1, int kMap_ = 0>
+template <int kThr_, int kGT_, int kMinW_, int kUF_ = kSplatU, int kNTPub_ = 1, int kMap_ = 0, int kTH_ = TH>
 struct SplatCfg {
     static constexpr int kThr = kThr_, kWaves = kThr_ / 64, kGT = kGT_, kMinW = kMinW_, kUF = kUF_, kNTPub = kNTPub_,
-                         kMap = kMap_;
+                         kMap = kMap_, kTH = kTH_;  // kTH: target tile height
 };
 
 // (image, tile) of linear index `lin` of the chunk's tile order
@@ -1016,8 +1024,8 @@ __device__ __forceinline__ void tile_of(unsigned lin, const ChunkArgs &a, const 
 // tile (txi, tyi), appended to L.seg; *cnt counts them (> kSegCap: too many,
 // the tile scans every block instead).  All loads of a thread in flight
 // together.
-template <typename Cfg>
-__device__ __forceinline__ void seg_scan(TileLds &L, unsigned *cnt, const ushort4 *segrec, const TileGeom &g, int txi,
+template <typename Cfg, typename Lds>
+__device__ __forceinline__ void seg_scan(Lds &L, unsigned *cnt, const ushort4 *segrec, const TileGeom &g, int txi,
                                          int tyi) {
     for (int s0 = threadIdx.x; s0 < g.nseg; s0 += Cfg::kThr * 4) {
         ushort4 r[4];
@@ -1061,9 +1069,10 @@ __device__ __forceinline__ unsigned dequeue_tile(unsigned *queue, unsigned home,
 // Every barrier is LDS-only: global loads are consumed by the thread that
 // issued them, and the published stores are never waited for.
 template <typename Coords, bool kVec, bool kFuse, bool kStamp, typename Cfg, typename E = float, bool kPack = false>
-__device__ __forceinline__ void splat_tile(TileLds &L, unsigned lin, int bl, int tile, const Coords &co,
+__device__ __forceinline__ void splat_tile(TileLdsT<Cfg::kTH> &L, unsigned lin, int bl, int tile, const Coords &co,
                                            const float *__restrict__ depth, const SplatIO &io, const ChunkArgs &a,
                                            int H, int W, int64_t HW, const TileGeom &g, unsigned long long *stamps) {
+    constexpr int TH = Cfg::kTH;  // this call's tile height (shadows the default)
     unsigned long long *ph = kStamp ? stamps + 8 * lin : nullptr;
     if constexpr (kStamp) { if (threadIdx.x == 0) ph[0] = wall_clock64(); }
 
@@ -1431,8 +1440,12 @@ using SplitCfg = SplatCfg<512, 2, 8>;  // split engine: 4 workgroups / CU, light
 #endif
 // targets in flight per thread, at most the tile's targets per thread (a
 // 128 x 16 tile at 512 threads holds 4 per thread)
-constexpr int gt_cap(int gt, int thr) { return gt < TW * TH / thr ? gt : TW * TH / thr; }
+constexpr int gt_cap(int gt, int thr, int th = TH) { return gt < TW * th / thr ? gt : TW * th / thr; }
 using FusedCfg = SplatCfg<OFD_PROBE_THR, gt_cap(OFD_PROBE_GT, OFD_PROBE_THR), OFD_PROBE_MINW, OFD_PROBE_UF>;
+// short calls (run_f32): 128 x 16 tiles, one workgroup per tile, 4 targets in
+// flight per thread (2048 targets / 512 threads)
+using FusedShortCfg = SplatCfg<OFD_PROBE_THR, gt_cap(OFD_PROBE_GT, OFD_PROBE_THR, kShortTH), OFD_PROBE_MINW, OFD_PROBE_UF,
+                               1, 0, kShortTH>;
 // coordinate sources that generate channels carry the generated values and a
 // division per source: 4 targets in flight keeps them inside 128 VGPRs
 // (Coords::kGenGT of them: 4 for the disparity source, 2 for the ego-motion
@@ -1453,7 +1466,7 @@ template <typename Coords, bool kVec, bool kFuse = false, bool kStamp = false, t
 __global__ __launch_bounds__(Cfg::kThr, Cfg::kMinW) void splat_kernel(Coords co, const float *__restrict__ depth,
                                                                 SplatIO io, ChunkArgs a, int H, int W, int64_t HW,
                                                                 TileGeom g, unsigned long long *stamps = nullptr) {
-    __shared__ TileLds L;
+    __shared__ TileLdsT<Cfg::kTH> L;
     const unsigned total = unsigned(a.nimg) * unsigned(g.ntiles);
     const unsigned per = (total + 7u) / 8u;
     const unsigned lin = (blockIdx.x % 8u) * per + blockIdx.x / 8u;
@@ -1477,7 +1490,7 @@ __global__ __launch_bounds__(Cfg::kThr, Cfg::kMinW) void splat_persist_kernel(Co
                                                                         SplatIO io, ChunkArgs a, int H, int W,
                                                                         int64_t HW, TileGeom g,
                                                                         unsigned long long *stamps = nullptr) {
-    __shared__ TileLds L;
+    __shared__ TileLdsT<Cfg::kTH> L;
     unsigned *queue = a.ws.queue;
     const unsigned total = unsigned(a.nimg) * unsigned(g.ntiles);
     const unsigned per = (total + 7u) / 8u;
@@ -1780,6 +1793,17 @@ unsigned persist_min() {
     return unsigned(g_persist_min);
 }
 
+// Short calls on 128 x kShortTH tiles (ofd_fw_set_short_tiles; OFD_FW_SHORT_TILES,
+// default on).  Results never depend on it.
+int g_short_tiles = -1;
+bool short_tiles_enabled() {
+    if (g_short_tiles < 0) {
+        const char *e = getenv("OFD_FW_SHORT_TILES");
+        g_short_tiles = (e && e[0] == '0') ? 0 : 1;
+    }
+    return g_short_tiles != 0;
+}
+
 // Optional timing hook (ofd_fw_set_profile_events): events recorded on the
 // launch stream right before the first and right after the last RESOLVE
 // launch of a call -- the dominant kernel -- so a benchmark can time it with
@@ -1821,7 +1845,7 @@ int run_f32(Coords co, const E *obj, const float *depth, E *out, float *valid, f
         const hipError_t e = hipMemsetAsync(ws, 0xFF, size_t(G) * per_image, st);
         if (e != hipSuccess) return int(e);
     }
-    const Ws slab = carve(ws, G, HW, g);
+    const Ws slab = carve(ws, G, HW, make_geom(H, W, kShortTH));  // the layout of both tile heights
     // 16-byte coordinate / depth loads in BIN and SPLAT
     const bool vec = W % 4 == 0 && co.vec_ok() && uintptr_t(depth) % 16 == 0;
     for (int64_t c = 0; c < nch; ++c) {
@@ -1852,11 +1876,28 @@ int run_f32(Coords co, const E *obj, const float *depth, E *out, float *valid, f
                 using Cfg = FusedCfgFor<Coords>;
                 auto fused = [&](auto vec_c, auto pack_c) {
                     constexpr bool kV = decltype(vec_c)::value, kP = decltype(pack_c)::value;
+                    const bool short_call = tiles < persist_min() * persist_slots<Coords, kV, Cfg, E, kP>();
                     if (c == 0 && g_prof_bin) (void)hipEventRecord(g_prof_bin, st);
+                    if constexpr (Coords::kGen == 0) {
+                        // short calls of plain coordinate sources: 128 x 16
+                        // tiles, twice the workgroups of the one-per-tile grid,
+                        // so the last tiles drain sooner (config 2: 0.154 ->
+                        // 0.150 ms, profiles/r06_t16_probe.txt)
+                        if (short_call && short_tiles_enabled()) {
+                            const TileGeom gs = make_geom(H, W, kShortTH);
+                            hipLaunchKernelGGL((bin_kernel<Coords, kV, kBinSPW, kP, kShortTH>), bgrid, dim3(kWarpThreads),
+                                               0, st, co, depth, a, int(H), int(W), HW, gs);
+                            if (c == 0 && g_prof_start) (void)hipEventRecord(g_prof_start, st);
+                            hipLaunchKernelGGL((splat_kernel<Coords, kV, true, false, FusedShortCfg, E, kP>),
+                                               dim3((unsigned(nb * gs.ntiles) + 7u) / 8u * 8u), dim3(FusedShortCfg::kThr),
+                                               0, st, co, depth, io, a, int(H), int(W), HW, gs, nullptr);
+                            return;
+                        }
+                    }
                     hipLaunchKernelGGL((bin_kernel<Coords, kV, kBinSPW, kP>), bgrid, dim3(kWarpThreads), 0, st, co,
                                        depth, a, int(H), int(W), HW, g);
                     if (c == 0 && g_prof_start) (void)hipEventRecord(g_prof_start, st);
-                    if (tiles < persist_min() * persist_slots<Coords, kV, Cfg, E, kP>())
+                    if (short_call)
                         hipLaunchKernelGGL((splat_kernel<Coords, kV, true, false, Cfg, E, kP>), sgrid, dim3(Cfg::kThr),
                                            0, st, co, depth, io, a, int(H), int(W), HW, g, nullptr);
                     else
@@ -2060,6 +2101,12 @@ int ofd_fw_set_disparity_rows(int on) {
 int ofd_fw_set_persist_min(int tiles_per_slot) {
     const int prev = int(persist_min());
     if (tiles_per_slot >= 0) g_persist_min = tiles_per_slot;
+    return prev;
+}
+
+int ofd_fw_set_short_tiles(int on) {
+    const int prev = short_tiles_enabled() ? 1 : 0;
+    if (on == 0 || on == 1) g_short_tiles = on;
     return prev;
 }
 

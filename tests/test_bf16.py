@@ -72,6 +72,28 @@ def test_bf16_warp_equals_f32_path_at_config5():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("short_tiles", [1, 0], ids=["tiles128x16", "tiles128x32"])
+def test_bf16_warp_config5_batch_bit_exact_vs_oracle(short_tiles):
+    """A config-5 call (16 images of 368x560, C=6, every bf16 bit pattern;
+    a short call: one SPLAT workgroup per tile) on both tile heights
+    (ofd_fw_set_short_tiles): the oracle's bits."""
+    from opticalflowfromdepth_amd import _native, forward_warp_flow
+    obj_bits, flow, depth = _case(16, 6, 368, 560, seed=5)
+    dev = torch.device("cuda:0")
+    lib = _native.lib()
+    prev = lib.ofd_fw_set_short_tiles(short_tiles)
+    try:
+        out, valid, coll = forward_warp_flow(_bits_to_bf16(obj_bits).to(dev), torch.from_numpy(flow).to(dev),
+                                             torch.from_numpy(depth).to(dev))
+        torch.cuda.synchronize()
+    finally:
+        lib.ofd_fw_set_short_tiles(prev)
+    e_out, e_valid, e_coll = _oracle_bf16(obj_bits, flow, depth)
+    assert np.array_equal(out.cpu().view(torch.int16).numpy().view(np.uint16), e_out)
+    assert np.array_equal(valid.cpu().numpy(), e_valid) and np.array_equal(coll.cpu().numpy(), e_coll)
+
+
+@pytest.mark.gpu
 def test_bf16_warp_argument_errors():
     from opticalflowfromdepth_amd import forward_warp_flow
     dev = torch.device("cuda:0")

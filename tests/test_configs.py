@@ -77,14 +77,23 @@ def test_config1_cpu_plumbing():
 
 
 @pytest.mark.gpu
-def test_config2_every_image_bit_exact(cuda_device):
+@pytest.mark.parametrize("short_tiles", [1, 0], ids=["tiles128x16", "tiles128x32"])
+def test_config2_every_image_bit_exact(cuda_device, short_tiles):
+    """Config 2 is a short call (4.7 tiles per resident SPLAT slot): by default
+    on 128 x 16 target tiles (ofd_fw_set_short_tiles), else 128 x 32 -- the
+    oracle's bits either way."""
     from oracle import oracle
-    from opticalflowfromdepth_amd import forward_warp_flow, synth
+    from opticalflowfromdepth_amd import _native, forward_warp_flow, synth
     B, H, W = 32, 480, 640
     obj, flow, depth = synth.stage_one_batch([12345 + i for i in range(B)], H, W, cuda_device)
     assert obj.shape == (B, 6, H, W)
-    out = forward_warp_flow(obj, flow, depth)
-    torch.cuda.synchronize()
+    lib = _native.lib()
+    prev = lib.ofd_fw_set_short_tiles(short_tiles)
+    try:
+        out = forward_warp_flow(obj, flow, depth)
+        torch.cuda.synchronize()
+    finally:
+        lib.ofd_fw_set_short_tiles(prev)
     exp = oracle.fw_flow(obj.cpu().numpy(), flow.cpu().numpy(), depth.cpu().numpy())
     for g, e, n in zip(out, exp, ("output", "valid", "collision")):
         g = g.cpu().numpy()

@@ -103,6 +103,17 @@ def test_schedule_setters_are_host_state():
     assert lib.ofd_fw_set_pack(1 - pk) == pk
     assert lib.ofd_fw_set_pack(7) == 1 - pk  # only queries
     lib.ofd_fw_set_pack(pk)
+    st = lib.ofd_fw_set_short_tiles(-1)
+    assert st in (0, 1)
+    assert lib.ofd_fw_set_short_tiles(1 - st) == st
+    assert lib.ofd_fw_set_short_tiles(7) == 1 - st  # only queries
+    lib.ofd_fw_set_short_tiles(st)
+    mw = lib.ofd_inpaint_seq_set_multi(0, 0)
+    assert 1 <= mw <= 16
+    assert lib.ofd_inpaint_seq_set_multi(3, 0) == mw
+    assert lib.ofd_inpaint_seq_set_multi(99, 0) == 3  # clamps to 16
+    assert lib.ofd_inpaint_seq_set_multi(-1, 0) == 16
+    lib.ofd_inpaint_seq_set_multi(mw, 0)
     pr = lib.ofd_inpaint_seq_set_pipeline(-1, -1, -1)
     assert pr >= 0
     assert lib.ofd_inpaint_seq_set_pipeline(5, 300, 0) == pr
