@@ -31,11 +31,12 @@
  *   ofd_inpaint_workspace_bytes, ofd_inpaint_seq_workspace_bytes
  *       no reference counterpart (cv2 allocates its fast-marching state per
  *       call); caller-owned scratch, no initialisation needed.
- *   ofd_inpaint_seq_set_groups, ofd_inpaint_seq_helper_device, ofd_inpaint_seq_set_pipeline
- *       no reference counterpart: how many stream-parallel groups the
- *       sequential fill splits a batch into (results never depend on it),
- *       the device whose helper streams a call would use, and the record /
- *       colour rounds pipelined beside the fast marches.
+ *   ofd_inpaint_seq_helper_device, ofd_inpaint_seq_set_pipeline,
+ *   ofd_inpaint_seq_set_colour, ofd_inpaint_seq_set_multi
+ *       no reference counterpart: the device whose helper stream a call
+ *       would use, the record / colour rounds pipelined beside the fast
+ *       marches, and the colour pass's form and workgroups per image
+ *       (results never depend on any of them).
  *   ofd_inpaint_set_schedule
  *       no reference counterpart: diagnostics / tests only (how many hole
  *       layers are launched one by one before the deep-tail
@@ -93,16 +94,6 @@ int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float 
                               int64_t B, int64_t C, int64_t H, int64_t W, int radius, void *workspace,
                               size_t workspace_bytes, void *stream);
 
-/* Sequential fill: split a batch into `groups` (1-4) groups of at least 2
- * images, run on the caller's stream and up to three library helper streams
- * (forked from and joined back into the caller's stream), each group in its
- * own slice of the workspace -- one group's colour pass then overlaps
- * another's fast march.  Applies when the whole batch fits the workspace as
- * one chunk.  Results never depend on it.  groups < 0 only queries; the
- * default comes from OFD_SEQ_GROUPS (else 1).  Process-wide;
- * returns the previous setting. */
-int ofd_inpaint_seq_set_groups(int groups);
-
 /* The pipelined sequential fill (radius 3, C <= 3 -- utils.inpaint's call --
  * on images of at least 2^18 pixels): `rounds` record / colour rounds run on
  * a helper stream beside the fast marches, `round_us` apart, over the holes
@@ -113,19 +104,8 @@ int ofd_inpaint_seq_set_groups(int groups);
  * pipelines smaller images too (tests).  Results never depend on any of it.
  * Negative values leave a setting as it is, round_us = 0 restores its
  * default; defaults OFD_SEQ_PIPE (else 12) and OFD_SEQ_PIPE_US (else 2000).
- * Process-wide; returns the previous number of rounds.  Grouped fills
- * (ofd_inpaint_seq_set_groups > 1) are not pipelined. */
+ * Process-wide; returns the previous number of rounds. */
 int ofd_inpaint_seq_set_pipeline(int rounds, int round_us, int force);
-
-/* Chip-wide early buckets of the sequential fill's two fast marches: up to
- * `buckets` buckets of each march run as launches over every march of the
- * chunk at once (the band- and ring-sized first buckets), until a march has
- * fewer than `min_pending` pending log entries; the march's own workgroup
- * takes over from there.  buckets = 0: off.  Results never depend on it.
- * Negative values leave a setting as it is; defaults OFD_SEQ_CW (else 0:
- * off, measured slower than the per-march workgroups) and 16384.
- * Process-wide; returns the previous number of buckets. */
-int ofd_inpaint_seq_set_chipwide(int buckets, int min_pending);
 
 /* The sequential fill's colour pass: mode 1 = levels-free (a hole is
  * coloured as soon as every earlier hole it reads is; no level barrier),

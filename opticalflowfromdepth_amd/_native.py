@@ -62,10 +62,8 @@ SIGNATURES = {
     "ofd_inpaint_set_schedule": ([ctypes.c_int, ctypes.c_int], ctypes.c_int),
     "ofd_inpaint_faults": ([ctypes.c_int], ctypes.c_int),
     "ofd_inpaint_tail_layers": ([ctypes.c_int], ctypes.c_int),
-    "ofd_inpaint_seq_set_groups": ([ctypes.c_int], ctypes.c_int),
     "ofd_inpaint_seq_helper_device": ([ctypes.c_void_p], ctypes.c_int),
     "ofd_inpaint_seq_set_pipeline": ([ctypes.c_int, ctypes.c_int, ctypes.c_int], ctypes.c_int),
-    "ofd_inpaint_seq_set_chipwide": ([ctypes.c_int, ctypes.c_int], ctypes.c_int),
     "ofd_inpaint_seq_set_colour": ([ctypes.c_int], ctypes.c_int),
     "ofd_inpaint_seq_set_multi": ([ctypes.c_int, ctypes.c_int], ctypes.c_int),
     "ofd_deflate_bound": ([_I64], _SZ),

@@ -119,9 +119,7 @@ struct SqWs {
     uint64_t *rq;    // radius-3 COLOUR: holes RECORD found ready (pixel << 32 | pixel)
     uint64_t *cy;    // radius-3 COLOUR: the frontier a time-bounded round carries to the next
     uint32_t *pipe;  // kPipe words per image: pipelined fill control (kP* below)
-    uint32_t *cw;    // chip-wide early buckets: per image, both marches' state and chunk counts
     int64_t en, eh, ew, hw;
-    int64_t cwn, cwstride;  // chunks per march (en / kCwCh, rounded up); cw words per image
 };
 
 // Pipelined fill control words (per image, kPipe words = two 128-byte lines
@@ -147,32 +145,12 @@ __device__ __forceinline__ void put64(uint32_t *p, uint64_t v) {
 constexpr uint32_t kK = 64;    // a hole is ready when its counter reaches kK (> 60 earlier holes)
 
 constexpr int kRecW = 40;  // record words: 32 weights (lane-major), 4 code words, dependants mask (2), weight sum, pad
-constexpr int kCwCh = 4096;  // chip-wide early buckets: the sorted run and the merge tile
-constexpr int kCwIt = 1024;  // ... items per chunk of the other phases
-constexpr int kCwSt = 32;    // ... and state words per march
-enum : int {
-    kSSeq = 0,      // log end
-    kSStart = 1,    // first push of buckets k-3 .. k (ring indexed by k & 3), 4 words
-    kSK = 5,        // the next bucket
-    kSN = 6,        // pops of the current bucket
-    kSNPush = 7,    // its pushes
-    kSDone = 8,     // the march is over
-    kSHand = 9,     // handed back to sq_fmm_kernel (small buckets)
-    kSLo = 10, kSHi = 11,  // the current bucket's candidates: log [lo, hi)
-    kSBk = 12,      // buckets with pops so far
-    kSBand = 13,    // the current bucket is the band (pops = log order)
-    kSNw = 14       // sweep worklist counters, 3 words (rotating)
-};
-__host__ __device__ constexpr int64_t cw_words(int64_t en) {  // per image: 2 x (state + chunk counts), 64-aligned
-    return (2 * kCwSt + 2 * ((en + kCwIt - 1) / kCwIt) + 63) / 64 * 64;
-}
 
 size_t per_image_bytes(int64_t H, int64_t W) {
     const size_t en = size_t(H + 2) * size_t(W + 2);
     return align256(en * 4) * 6 + align256(en * 8) * 2 + align256(size_t(H + 2) * 4) + kMeta * 4 +
            en * kRecW * 4 + size_t(H) * size_t(W) * 4 + en * 8 + 3 * 256 +
-           en * 8 + en * 4 * 6 + en * 4 * 2 + en * 4 + en * 8 + en * 8 + kPipe * 4 + size_t(cw_words(int64_t(en))) * 4 +
-           8 * 256;
+           en * 8 + en * 4 * 6 + en * 4 * 2 + en * 4 + en * 8 + en * 8 + kPipe * 4 + 8 * 256;
 }
 
 SqWs carve(void *ws, int64_t G, int64_t H, int64_t W) {
@@ -202,10 +180,7 @@ SqWs carve(void *ws, int64_t G, int64_t H, int64_t W) {
     w.kc = reinterpret_cast<uint32_t *>(p), p += align256(size_t(G) * size_t(w.en) * 4);
     w.rq = reinterpret_cast<uint64_t *>(p), p += align256(size_t(G) * size_t(w.en) * 8);
     w.cy = reinterpret_cast<uint64_t *>(p), p += align256(size_t(G) * size_t(w.en) * 8);
-    w.pipe = reinterpret_cast<uint32_t *>(p), p += align256(size_t(G) * kPipe * 4);
-    w.cwn = (w.en + kCwIt - 1) / kCwIt;
-    w.cwstride = cw_words(w.en);
-    w.cw = reinterpret_cast<uint32_t *>(p);
+    w.pipe = reinterpret_cast<uint32_t *>(p);
     return w;
 }
 
@@ -797,11 +772,9 @@ __device__ __forceinline__ void publish_prog(const Img &m, uint32_t seq, uint64_
     __hip_atomic_store(&m.pipe[kPProg], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// cs: the state the chip-wide early buckets left (sq_cw_*), or null: the
-// march resumes at the bucket they stopped at.
 template <bool kInner>
 __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L, uint32_t &nbuckets, uint64_t *prof,
-                         double bscale, bool pub, const uint32_t *cs) {
+                         double bscale, bool pub) {
     (void)prof;
     uint64_t last_pub = 0;
     const int tid = threadIdx.x, ew = m.ew;
@@ -809,15 +782,7 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
     uint32_t seq = nb;
     uint32_t start[4] = {nb, nb, nb, nb};  // first push of buckets k-3 .. k (ring indexed by k & 3)
     nbuckets = 0;
-    uint32_t kfirst = 0;
-    if (cs) {
-        nbuckets = cs[kSBk];
-        if (cs[kSDone]) return cs[kSSeq];
-        seq = cs[kSSeq];
-        for (int i = 0; i < 4; ++i) start[i] = cs[kSStart + i];
-        kfirst = cs[kSK];
-    }
-    for (uint32_t k = kfirst;; ++k) {
+    for (uint32_t k = 0;; ++k) {
         uint32_t lo, hi = seq;
         if (k == 0) {
             lo = 0;
@@ -1172,613 +1137,15 @@ __device__ __forceinline__ Img outer_view(const Img &m) {
     return o;
 }
 
-// ---------------------------------------------------------------- chip-wide early buckets
-// The first buckets of both marches are large: the band and the ring, up to
-// ~200 k pops per image, 1.7-4.7 ms each on the march's one workgroup
-// (profiles/r04_seq_bucket_trace.txt), and the outer march is nothing else.
-// They gate the first records and so the colour chain.  Here they run as
-// launches over every march of the chunk at once (march z: image z >> 1,
-// z & 1 = 0 the outer march, 1 the inner), one kernel per phase of
-// fmm_pass's bucket step, with fmm_pass's results: pops in (T, push seq)
-// order (ordered compaction of the bucket, LDS-sorted 4096-key runs merged
-// by merge path), claims by atomicMin of rank * 4 + direction, pushes
-// numbered in (rank, direction) order by an ordered scan, distance sweeps
-// to the fixed point, the log's distances.  A march whose pending entries
-// drop below a threshold is handed back; sq_fmm_kernel resumes every march
-// from the state left here (cw words).  Kernel boundaries order the phases
-// (a sweep reads neighbours another workgroup may be updating: a stale read
-// only gives a value the changed neighbour's re-queue corrects next sweep).
-constexpr int kCwT = 256;                  // threads per chunk workgroup
-constexpr int kCwPer = kCwIt / kCwT;       // items per thread, loads issued together
-constexpr uint32_t kCwMinDefault = 16384;  // pending entries below which a march goes back to its workgroup
-constexpr int kCwSweeps = 12;              // sweep launches per bucket (the rest: one workgroup per march)
-constexpr int kCwGrid = 2048;              // workgroups of a chunk kernel
-constexpr int kCwMaxSegs = 2048;           // marches per chunk the launches handle (else no chip-wide buckets)
-
-struct CwSeg {
-    uint32_t *st, *logp, *own, *s, *cnt, *meta, *px;
-    float *logt, *t;
-    uint64_t *k0, *k1;
-    int ew;
-    bool inner;
-    uint32_t nb;
-};
-
-__device__ __forceinline__ uint32_t *cw_state(const SqWs &w, int z) {
-    return w.cw + int64_t(z >> 1) * w.cwstride + ((z & 1) ? kCwSt : 0);
-}
-
-__device__ __forceinline__ CwSeg cw_seg(const SqWs &w, int z) {
-    const Img m = image(w, z >> 1);
-    const bool inner = (z & 1) != 0;
-    const Img v = inner ? m : outer_view(m);
-    CwSeg g;
-    g.st = inner ? m.sI : m.sO;
-    g.logp = v.logp;
-    g.logt = v.logt;
-    g.k0 = v.k0;
-    g.k1 = v.k1;
-    g.px = m.rpx + (inner ? 0 : m.en);  // the pops' pixels by rank (the sort's last pass)
-    g.own = m.own;
-    g.t = m.t;
-    g.meta = m.meta;
-    g.ew = m.ew;
-    g.inner = inner;
-    g.nb = m.meta[0];
-    g.s = cw_state(w, z);
-    g.cnt = w.cw + int64_t(z >> 1) * w.cwstride + 2 * kCwSt + (inner ? w.cwn : 0);
-    return g;
-}
-
-// skipped by this bucket's chip-wide kernels
-__device__ __forceinline__ bool cw_idle(const uint32_t *s) { return s[kSDone] | s[kSHand]; }
-__device__ __forceinline__ uint32_t cdiv(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
-
-// exclusive scan over the kCwT-thread workgroup (ws: kCwT / 64 LDS words)
-__device__ __forceinline__ uint32_t cw_scan(uint32_t v, uint32_t &tot, uint32_t *ws) {
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    uint32_t x = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d);
-        if (lane >= d) x += y;
-    }
-    if (lane == 63) ws[wv] = x;
-    __syncthreads();
-    uint32_t off = 0, t = 0;
-#pragma unroll
-    for (int i = 0; i < kCwT / 64; ++i) {
-        const uint32_t q = ws[i];
-        off += i < wv ? q : 0u;
-        t += q;
-    }
-    __syncthreads();
-    tot = t;
-    return off + x - v;
-}
-
-// A chunk kernel's items: chunk c of march z for c < ext(state of z).  Each
-// workgroup puts the inclusive prefix of the marches' chunk counts in LDS
-// once and strides over the real items only (a march has many chunks in its
-// band-sized buckets, few or none later).
-struct CwPlan {
-    uint32_t pre[kCwMaxSegs];
-    uint32_t ws[kCwT / 64];
-};
-template <typename Ext>
-__device__ __forceinline__ uint32_t cw_plan(const SqWs &w, int segs, CwPlan &P, Ext ext) {
-    uint32_t carry = 0;
-    for (int z0 = 0; z0 < segs; z0 += kCwT) {
-        const int z = z0 + int(threadIdx.x);
-        const uint32_t e = z < segs ? ext(cw_state(w, z)) : 0u;
-        uint32_t tot;
-        const uint32_t ex = cw_scan(e, tot, P.ws);
-        if (z < segs) P.pre[z] = carry + ex + e;
-        carry += tot;
-    }
-    __syncthreads();
-    return carry;
-}
-__device__ __forceinline__ void cw_item(const CwPlan &P, int segs, uint32_t item, int &z, uint32_t &c) {
-    int lo = 0, hi = segs - 1;
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (P.pre[mid] > item)
-            hi = mid;
-        else
-            lo = mid + 1;
-    }
-    z = lo;
-    c = item - (lo ? P.pre[lo - 1] : 0u);
-}
-#define CW_ITEMS(P, total)                                                                                     \
-    for (uint32_t item_ = blockIdx.x; item_ < (total); item_ += gridDim.x)                                     \
-        if (int z_ = 0; true)                                                                                  \
-            if (uint32_t c_ = 0; (cw_item(P, segs, item_, z_, c_), true))
-
-// bucket k's start (fmm_pass's loop head), one thread per march
-__global__ __launch_bounds__(64) void sq_cw_begin_kernel(SqWs w, int k, uint32_t min_pending) {
-    if (threadIdx.x) return;
-    const CwSeg g = cw_seg(w, blockIdx.x);
-    uint32_t *s = g.s;
-    if (k == 0) {
-        for (int i = 0; i < kCwSt; ++i) s[i] = 0u;
-        s[kSSeq] = g.nb;
-        for (int i = 0; i < 4; ++i) s[kSStart + i] = g.nb;
-        if (g.nb == 0) {
-            s[kSDone] = 1u;
-            return;
-        }
-        s[kSHi] = g.nb;
-        s[kSN] = g.nb;  // the band: every log entry, already in (T, seq) order
-        s[kSBand] = 1u;
-        return;
-    }
-    if (cw_idle(s)) return;
-    const uint32_t seq = s[kSSeq];
-    const uint32_t lo = k >= 3 ? s[kSStart + ((k - 3) & 3)] : g.nb;
-    s[kSK] = uint32_t(k);
-    if (lo == seq) {  // nothing pending
-        s[kSDone] = 1u;
-        return;
-    }
-    if (seq - lo < min_pending) {  // small from here on: back to the march's workgroup, at bucket k
-        s[kSHand] = 1u;
-        return;
-    }
-    s[kSStart + (k & 3)] = seq;
-    s[kSNw] = s[kSNw + 1] = s[kSNw + 2] = 0u;
-    s[kSLo] = lo;
-    s[kSHi] = seq;
-    s[kSN] = 0u;
-    s[kSNPush] = 0u;
-    s[kSBand] = 0u;
-}
-
-__device__ __forceinline__ uint32_t cw_ext_cand(const uint32_t *s) {  // chunks of the bucket's candidates
-    return (cw_idle(s) || s[kSBand]) ? 0u : cdiv(s[kSHi] - s[kSLo], kCwIt);
-}
-
-// entries of bucket k per chunk of the candidates
-__global__ __launch_bounds__(kCwT) void sq_cw_select_kernel(SqWs w, int segs, int k, double bscale) {
-    __shared__ CwPlan P;
-    __shared__ uint32_t tot;
-    const uint32_t total = cw_plan(w, segs, P, cw_ext_cand);
-    CW_ITEMS(P, total) {
-        const CwSeg g = cw_seg(w, z_);
-        const uint32_t lo = g.s[kSLo], hi = g.s[kSHi], c0 = lo + c_ * kCwIt;
-        if (threadIdx.x == 0) tot = 0u;
-        float T[kCwPer];
-#pragma unroll
-        for (int u = 0; u < kCwPer; ++u) {
-            const uint32_t i = c0 + uint32_t(u * kCwT) + threadIdx.x;
-            T[u] = i < hi ? g.logt[i] : -1.f;
-        }
-        uint32_t c = 0;
-#pragma unroll
-        for (int u = 0; u < kCwPer; ++u) c += (T[u] >= 0.f && bucket_of(T[u], bscale) == uint32_t(k)) ? 1u : 0u;
-        __syncthreads();
-        atomicAdd(&tot, c);
-        __syncthreads();
-        if (threadIdx.x == 0) g.cnt[c_] = tot;
-    }
-}
-
-// exclusive scan of the chunk counts, one workgroup per march; which = 0:
-// the bucket's pops (candidates' chunks), 1: its pushes (ranks' chunks)
-__global__ __launch_bounds__(kCwT) void sq_cw_scan_kernel(SqWs w, int which) {
-    __shared__ uint32_t ws[kCwT / 64];
-    const CwSeg g = cw_seg(w, blockIdx.x);
-    uint32_t *s = g.s;
-    if (cw_idle(s) || (which == 0 && s[kSBand])) return;
-    const uint32_t len = which == 0 ? s[kSHi] - s[kSLo] : s[kSN];
-    const uint32_t nch = cdiv(len, kCwIt);
-    uint32_t carry = 0;
-    for (uint32_t c0 = 0; c0 < nch; c0 += kCwT) {
-        const uint32_t c = c0 + threadIdx.x;
-        uint32_t tot;
-        const uint32_t ex = cw_scan(c < nch ? g.cnt[c] : 0u, tot, ws);
-        if (c < nch) g.cnt[c] = carry + ex;
-        carry += tot;
-    }
-    if (threadIdx.x == 0) s[which == 0 ? kSN : kSNPush] = carry;
-}
-
-// the bucket's keys (distance bits << 32 | log index) in log order: each
-// thread's kCwPer consecutive candidates, one ordered scan per chunk
-__global__ __launch_bounds__(kCwT) void sq_cw_write_kernel(SqWs w, int segs, int k, double bscale) {
-    __shared__ CwPlan P;
-    const uint32_t total = cw_plan(w, segs, P, cw_ext_cand);
-    CW_ITEMS(P, total) {
-        const CwSeg g = cw_seg(w, z_);
-        const uint32_t lo = g.s[kSLo], hi = g.s[kSHi], i0 = lo + c_ * kCwIt + threadIdx.x * kCwPer;
-        float T[kCwPer];
-        unsigned sel = 0;
-#pragma unroll
-        for (int u = 0; u < kCwPer; ++u) {
-            T[u] = i0 + u < hi ? g.logt[i0 + u] : -1.f;
-            if (T[u] >= 0.f && bucket_of(T[u], bscale) == uint32_t(k)) sel |= 1u << u;
-        }
-        uint32_t tot;
-        uint32_t pos = g.cnt[c_] + cw_scan(uint32_t(__popc(sel)), tot, P.ws);
-#pragma unroll
-        for (int u = 0; u < kCwPer; ++u)  // -0 -> +0: the heap compares values
-            if (sel & (1u << u)) g.k0[pos++] = (uint64_t(__float_as_uint(T[u] + 0.0f)) << 32) | (i0 + u);
-    }
-}
-
-// sort each run of kCwCh keys in LDS (bitonic); a bucket of one run is
-// final here: its pops' pixels by rank too
-__global__ __launch_bounds__(kCwT) void sq_cw_runsort_kernel(SqWs w, int segs) {
-    __shared__ CwPlan P;
-    __shared__ uint64_t K[kCwCh];
-    const uint32_t total = cw_plan(w, segs, P, [](const uint32_t *s) {
-        return (cw_idle(s) || s[kSBand]) ? 0u : cdiv(s[kSN], kCwCh);
-    });
-    CW_ITEMS(P, total) {
-        const CwSeg g = cw_seg(w, z_);
-        const uint32_t n = g.s[kSN], r0 = c_ * kCwCh, len = min(uint32_t(kCwCh), n - r0);
-        uint32_t m2 = 64;
-        while (m2 < len) m2 <<= 1;  // power of two >= len (uniform)
-        __syncthreads();            // K of the item before
-        for (uint32_t i = threadIdx.x; i < m2; i += kCwT) K[i] = i < len ? g.k0[r0 + i] : ~uint64_t(0);
-        __syncthreads();
-        for (uint32_t kk = 2; kk <= m2; kk <<= 1)
-            for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
-                for (uint32_t i = threadIdx.x; i < m2; i += kCwT) {
-                    const uint32_t ixj = i ^ j;
-                    if (ixj > i) {
-                        const uint64_t a = K[i], b = K[ixj];
-                        if ((a > b) == ((i & kk) == 0)) {
-                            K[i] = b;
-                            K[ixj] = a;
-                        }
-                    }
-                }
-                __syncthreads();
-            }
-        const bool last = n <= uint32_t(kCwCh);
-        for (uint32_t i = threadIdx.x; i < len; i += kCwT) {
-            g.k0[r0 + i] = K[i];
-            if (last) g.px[r0 + i] = g.logp[uint32_t(K[i])];
-        }
-    }
-}
-
-// merge pass p: sorted runs of kCwCh << p keys into runs of twice that.
-// Workgroup = one output tile of kCwCh keys: its split of the two input runs
-// by merge path (binary search on the tile's first and last diagonal), the
-// two slices in LDS, each key placed at its index plus its rank in the other
-// slice (keys are unique).  The last pass of a bucket also writes its pops'
-// pixels by rank.
-__global__ __launch_bounds__(kCwT) void sq_cw_merge_kernel(SqWs w, int segs, int p) {
-    __shared__ CwPlan P;
-    __shared__ uint64_t A[kCwCh];
-    __shared__ uint32_t split[2];
-    const uint32_t wd = uint32_t(kCwCh) << p;
-    const uint32_t total = cw_plan(w, segs, P, [wd](const uint32_t *s) {
-        return (cw_idle(s) || s[kSBand] || s[kSN] <= wd) ? 0u : cdiv(s[kSN], kCwCh);
-    });
-    CW_ITEMS(P, total) {
-        const CwSeg g = cw_seg(w, z_);
-        const uint32_t n = g.s[kSN], o0 = c_ * kCwCh;
-        const uint64_t *src = (p & 1) ? g.k1 : g.k0;
-        uint64_t *dst = (p & 1) ? g.k0 : g.k1;
-        const uint32_t plo = o0 / (2 * wd) * (2 * wd), pmid = min(plo + wd, n), phi = min(plo + 2 * wd, n);
-        const uint32_t o1 = min(o0 + uint32_t(kCwCh), phi), la = pmid - plo, lb = phi - pmid;
-        const uint64_t *Ap = src + plo, *Bp = src + pmid;
-        __syncthreads();  // split and A of the item before
-        if (threadIdx.x < 2) {
-            const uint32_t d = (threadIdx.x == 0 ? o0 : o1) - plo;
-            uint32_t a = d > lb ? d - lb : 0u, b = min(d, la);
-            while (a < b) {
-                const uint32_t mid = (a + b) >> 1;
-                if (Ap[mid] < Bp[d - 1 - mid])
-                    a = mid + 1;
-                else
-                    b = mid;
-            }
-            split[threadIdx.x] = a;
-        }
-        __syncthreads();
-        const uint32_t a0 = split[0], a1 = split[1];
-        const uint32_t b0 = (o0 - plo) - a0, na = a1 - a0, nt = o1 - o0, nbk = nt - na;
-        for (uint32_t i = threadIdx.x; i < nt; i += kCwT) A[i] = i < na ? Ap[a0 + i] : Bp[b0 + (i - na)];
-        __syncthreads();
-        const bool last = n <= 2 * wd;
-        for (uint32_t i = threadIdx.x; i < nt; i += kCwT) {
-            const uint64_t key = A[i];
-            const uint32_t pos = i < na ? i + lower_bound64(A + na, nbk, key) : (i - na) + lower_bound64(A, na, key);
-            dst[o0 + pos] = key;
-            if (last) g.px[o0 + pos] = g.logp[uint32_t(key)];
-        }
-    }
-}
-
-__device__ __forceinline__ uint32_t cw_ext_pops(const uint32_t *s) {  // chunks of the bucket's ranks
-    return cw_idle(s) ? 0u : cdiv(s[kSN], kCwIt);
-}
-
-// the pixel of pop r (the band's pops are the log itself)
-__device__ __forceinline__ int64_t cw_pop(const CwSeg &g, bool band, uint32_t r) {
-    return int64_t(band ? g.logp[r] : g.px[r]);
-}
-
-// claims: the INSIDE neighbours of every pop, first claimant (rank * 4 + q) wins
-__global__ __launch_bounds__(kCwT) void sq_cw_claim_kernel(SqWs w, int segs) {
-    __shared__ CwPlan P;
-    const uint32_t total = cw_plan(w, segs, P, cw_ext_pops);
-    CW_ITEMS(P, total) {
-        const CwSeg g = cw_seg(w, z_);
-        const uint32_t n = g.s[kSN], r0 = c_ * kCwIt;
-        const bool band = g.s[kSBand] != 0u;
-        const int64_t off[4] = {-int64_t(g.ew), -1, int64_t(g.ew), 1};
-        int64_t a[kCwPer];
-        uint32_t sv[kCwPer][4];
-#pragma unroll
-        for (int u = 0; u < kCwPer; ++u) {
-            const uint32_t r = r0 + uint32_t(u * kCwT) + threadIdx.x;
-            a[u] = r < n ? cw_pop(g, band, r) : -1;
-        }
-#pragma unroll
-        for (int u = 0; u < kCwPer; ++u)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) sv[u][q] = a[u] >= 0 ? g.st[a[u] + off[q]] : 0u;
-#pragma unroll
-        for (int u = 0; u < kCwPer; ++u)
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                if (sv[u][q] == INF)
-                    atomicMin(&g.own[a[u] + off[q]], (r0 + uint32_t(u * kCwT) + threadIdx.x) * 4u + uint32_t(q));
-    }
-}
-
-// the pushes (claims won) of this thread's pops: rank r0 + u * stride, as
-// direction masks
-__device__ __forceinline__ void cw_mine(const CwSeg &g, bool band, uint32_t n, uint32_t r0, uint32_t stride,
-                                        int64_t (&a)[kCwPer], unsigned (&mine)[kCwPer]) {
-    const int64_t off[4] = {-int64_t(g.ew), -1, int64_t(g.ew), 1};
-    uint32_t sv[kCwPer][4], ov[kCwPer][4];
-#pragma unroll
-    for (int u = 0; u < kCwPer; ++u) {
-        const uint32_t r = r0 + uint32_t(u) * stride;
-        a[u] = r < n ? cw_pop(g, band, r) : -1;
-    }
-#pragma unroll
-    for (int u = 0; u < kCwPer; ++u)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            sv[u][q] = a[u] >= 0 ? g.st[a[u] + off[q]] : 0u;
-            ov[u][q] = a[u] >= 0 ? g.own[a[u] + off[q]] : 0u;
-        }
-#pragma unroll
-    for (int u = 0; u < kCwPer; ++u) {
-        mine[u] = 0;
-        const uint32_t r = r0 + uint32_t(u) * stride;
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-            if (sv[u][q] == INF && ov[u][q] == r * 4u + uint32_t(q)) mine[u] |= 1u << q;
-    }
-}
-
-// pushes per chunk of ranks
-__global__ __launch_bounds__(kCwT) void sq_cw_pcount_kernel(SqWs w, int segs) {
-    __shared__ CwPlan P;
-    __shared__ uint32_t tot;
-    const uint32_t total = cw_plan(w, segs, P, cw_ext_pops);
-    CW_ITEMS(P, total) {
-        const CwSeg g = cw_seg(w, z_);
-        const uint32_t n = g.s[kSN];
-        int64_t a[kCwPer];
-        unsigned mine[kCwPer];
-        cw_mine(g, g.s[kSBand] != 0u, n, c_ * kCwIt + threadIdx.x, kCwT, a, mine);
-        uint32_t c = 0;
-#pragma unroll
-        for (int u = 0; u < kCwPer; ++u) c += uint32_t(__popc(mine[u]));
-        if (threadIdx.x == 0) tot = 0u;
-        __syncthreads();
-        atomicAdd(&tot, c);
-        __syncthreads();
-        if (threadIdx.x == 0) g.cnt[c_] = tot;
-        __syncthreads();
-    }
-}
-
-// pushes numbered in (rank, direction) order (each thread's kCwPer
-// consecutive ranks): stamps and log pixels
-__global__ __launch_bounds__(kCwT) void sq_cw_push_kernel(SqWs w, int segs) {
-    __shared__ CwPlan P;
-    const uint32_t total = cw_plan(w, segs, P, cw_ext_pops);
-    CW_ITEMS(P, total) {
-        const CwSeg g = cw_seg(w, z_);
-        const uint32_t n = g.s[kSN], seq = g.s[kSSeq];
-        const int64_t off[4] = {-int64_t(g.ew), -1, int64_t(g.ew), 1};
-        int64_t a[kCwPer];
-        unsigned mine[kCwPer];
-        cw_mine(g, g.s[kSBand] != 0u, n, c_ * kCwIt + threadIdx.x * kCwPer, 1, a, mine);
-        uint32_t c = 0;
-#pragma unroll
-        for (int u = 0; u < kCwPer; ++u) c += uint32_t(__popc(mine[u]));
-        uint32_t tot;
-        uint32_t pos = seq + g.cnt[c_] + cw_scan(c, tot, P.ws);
-#pragma unroll
-        for (int u = 0; u < kCwPer; ++u)
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                if (mine[u] & (1u << q)) {
-                    const int64_t px = a[u] + off[q];
-                    g.st[px] = pos;
-                    g.logp[pos] = uint32_t(px);
-                    ++pos;
-                }
-    }
-}
-
-// Distance sweep over items (sweep 0: every push of the bucket; later
-// sweeps: the worklist of pushes next to one whose distance changed),
-// queueing the later pushes of this bucket next to each change (deduplicated
-// by a per-sweep tag in own[], as in fmm_pass), with one atomic per wave.
-// Every lane of the wave calls it; x[u] valid where act bit u is set.
-template <bool kInner>
-__device__ __forceinline__ void cw_sweep_items(const CwSeg &g, uint32_t seq, const uint32_t (&x)[kCwPer], unsigned act,
-                                               uint32_t tag, uint32_t *wb, uint32_t *nwb) {
-    const int64_t off[4] = {-int64_t(g.ew), -1, int64_t(g.ew), 1};
-    int64_t p[kCwPer];
-#pragma unroll
-    for (int u = 0; u < kCwPer; ++u) p[u] = (act >> u) & 1u ? int64_t(g.logp[seq + x[u]]) : 0;
-    float T[kCwPer], cur[kCwPer];
-#pragma unroll
-    for (int u = 0; u < kCwPer; ++u) {
-        const bool on = (act >> u) & 1u;
-        T[u] = on ? fm_dist_seq<kInner>(g.st, g.t, p[u], g.ew, seq + x[u]) : 0.f;
-        cur[u] = on ? g.t[p[u]] : 0.f;
-    }
-    uint32_t add[4 * kCwPer];
-    uint32_t na = 0;
-#pragma unroll
-    for (int u = 0; u < kCwPer; ++u)
-        if (((act >> u) & 1u) && T[u] != cur[u]) {
-            g.t[p[u]] = T[u];
-            const uint32_t sp = seq + x[u];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int64_t nq = p[u] + off[q];
-                const uint32_t sn = g.st[nq];
-                if (sn > sp && sn != INF && atomicExch(&g.own[nq], tag) != tag) add[na++] = sn - seq;
-            }
-        }
-    const int lane = threadIdx.x & 63;
-    uint32_t x2 = na;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(x2, d);
-        if (lane >= d) x2 += y;
-    }
-    const uint32_t tot = __shfl(x2, 63);
-    uint32_t base = 0;
-    if (lane == 63 && tot) base = atomicAdd(nwb, tot);
-    base = __shfl(base, 63) + x2 - na;
-    for (uint32_t e = 0; e < na; ++e) wb[base + e] = add[e];
-}
-
-__global__ __launch_bounds__(kCwT) void sq_cw_sweep_kernel(SqWs w, int segs, int it) {
-    __shared__ CwPlan P;
-    // the next sweep's queue counter (nobody reads or appends to it in this sweep)
-    if (blockIdx.x == 0)
-        for (int z = threadIdx.x; z < segs; z += kCwT) cw_state(w, z)[kSNw + (it + 1) % 3] = 0u;
-    const uint32_t total = cw_plan(w, segs, P, [it](const uint32_t *s) {
-        return cw_idle(s) ? 0u : cdiv(it == 0 ? s[kSNPush] : s[kSNw + (it + 2) % 3], kCwIt);
-    });
-    const uint32_t tag = 0x80000000u | uint32_t(it);
-    CW_ITEMS(P, total) {
-        const CwSeg g = cw_seg(w, z_);
-        uint32_t *s = g.s;
-        const uint32_t nw = it == 0 ? s[kSNPush] : s[kSNw + (it + 2) % 3], seq = s[kSSeq];
-        const uint32_t *wa = reinterpret_cast<const uint32_t *>((it & 1) ? g.k0 : g.k1);
-        uint32_t *wb = reinterpret_cast<uint32_t *>((it & 1) ? g.k1 : g.k0);
-        uint32_t x[kCwPer];
-        unsigned act = 0;
-#pragma unroll
-        for (int u = 0; u < kCwPer; ++u) {
-            const uint32_t i = c_ * kCwIt + uint32_t(u * kCwT) + threadIdx.x;
-            x[u] = 0u;
-            if (i < nw) {
-                x[u] = it == 0 ? i : wa[i];
-                act |= 1u << u;
-            }
-        }
-        if (g.inner)
-            cw_sweep_items<true>(g, seq, x, act, tag, wb, &s[kSNw + it % 3]);
-        else
-            cw_sweep_items<false>(g, seq, x, act, tag, wb, &s[kSNw + it % 3]);
-    }
-}
-
-// the sweeps past kCwSweeps, one workgroup per march, to the fixed point
-__global__ __launch_bounds__(kCwT) void sq_cw_sweep_rest_kernel(SqWs w) {
-    const CwSeg g = cw_seg(w, blockIdx.x);
-    uint32_t *s = g.s;
-    if (cw_idle(s)) return;
-    const uint32_t np = s[kSNPush], seq = s[kSSeq];
-    for (uint32_t it = kCwSweeps;; ++it) {
-        const uint32_t nw = s[kSNw + (it + 2) % 3];
-        if (nw == 0) break;  // uniform: read after the barrier that ended the sweep before
-        if (it > np + 1) {
-            if (threadIdx.x == 0) {
-                g.meta[5] = 2u;
-                atomicOr(&g_sq_fault, 4u);
-            }
-            break;
-        }
-        sync_all();  // every thread has read nw before the reset below
-        if (threadIdx.x == 0) s[kSNw + (it + 1) % 3] = 0u;
-        const uint32_t tag = 0x80000000u | it;
-        const uint32_t *wa = reinterpret_cast<const uint32_t *>((it & 1) ? g.k0 : g.k1);
-        uint32_t *wb = reinterpret_cast<uint32_t *>((it & 1) ? g.k1 : g.k0);
-        for (uint32_t i0 = 0; i0 < nw; i0 += kCwIt) {
-            uint32_t x[kCwPer];
-            unsigned act = 0;
-#pragma unroll
-            for (int u = 0; u < kCwPer; ++u) {
-                const uint32_t i = i0 + uint32_t(u * kCwT) + threadIdx.x;
-                x[u] = i < nw ? wa[i] : 0u;
-                act |= (i < nw ? 1u : 0u) << u;
-            }
-            if (g.inner)
-                cw_sweep_items<true>(g, seq, x, act, tag, wb, &s[kSNw + it % 3]);
-            else
-                cw_sweep_items<false>(g, seq, x, act, tag, wb, &s[kSNw + it % 3]);
-        }
-        sync_all();
-    }
-}
-
-// the pushes' distances into the log
-__global__ __launch_bounds__(kCwT) void sq_cw_log_kernel(SqWs w, int segs) {
-    __shared__ CwPlan P;
-    const uint32_t total =
-        cw_plan(w, segs, P, [](const uint32_t *s) { return cw_idle(s) ? 0u : cdiv(s[kSNPush], kCwIt); });
-    CW_ITEMS(P, total) {
-        const CwSeg g = cw_seg(w, z_);
-        const uint32_t np = g.s[kSNPush], seq = g.s[kSSeq];
-        uint32_t p[kCwPer];
-#pragma unroll
-        for (int u = 0; u < kCwPer; ++u) {
-            const uint32_t i = c_ * kCwIt + uint32_t(u * kCwT) + threadIdx.x;
-            p[u] = i < np ? g.logp[seq + i] : 0u;
-        }
-        float T[kCwPer];
-#pragma unroll
-        for (int u = 0; u < kCwPer; ++u) T[u] = g.t[p[u]];
-#pragma unroll
-        for (int u = 0; u < kCwPer; ++u) {
-            const uint32_t i = c_ * kCwIt + uint32_t(u * kCwT) + threadIdx.x;
-            if (i < np) g.logt[seq + i] = T[u];
-        }
-    }
-}
-
-// bucket k done: advance the log end
-__global__ __launch_bounds__(64) void sq_cw_end_kernel(SqWs w, int k) {
-    if (threadIdx.x) return;
-    const CwSeg g = cw_seg(w, blockIdx.x);
-    uint32_t *s = g.s;
-    if (cw_idle(s)) return;
-    s[kSSeq] += s[kSNPush];
-    s[kSBk] += s[kSN] ? 1u : 0u;
-    s[kSK] = uint32_t(k + 1);
-}
-
 // Two workgroups per image: blockIdx.y = 0 runs the outer march over the ring
 // (icvCalcFMM(out, t, Out, negate = true)) and negates its distances,
 // blockIdx.y = 1 the inner march over the holes (icvTeleaInpaintFMM's order).
 // They touch disjoint pixels (ring pixels are not 4-adjacent to holes) and
 // keep separate stamps, logs and sort buffers; the only value both read is
 // the band's zero distance (band_t).
-__global__ __launch_bounds__(kThreads) void sq_fmm_kernel(SqWs w, double bscale, int pub, int cw) {
+__global__ __launch_bounds__(kThreads) void sq_fmm_kernel(SqWs w, double bscale, int pub) {
     __shared__ FmmLds L;
     const Img m = image(w, blockIdx.x);
-    const uint32_t *cs = w.cw + int64_t(blockIdx.x) * w.cwstride;  // the chip-wide buckets' state (cw != 0)
     const uint32_t nb = m.meta[0];
     uint32_t nbk = 0;
     uint64_t prof[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -1789,7 +1156,7 @@ __global__ __launch_bounds__(kThreads) void sq_fmm_kernel(SqWs w, double bscale,
     if (threadIdx.x == 0 && blockIdx.y == 1) put64(m.pipe + kPTFmm, w0);
     if (blockIdx.y == 0) {
         const Img o = outer_view(m);
-        const uint32_t no = fmm_pass<false>(o, m.sO, nb, L, nbk, prof, bscale, false, cw ? cs : nullptr);
+        const uint32_t no = fmm_pass<false>(o, m.sO, nb, L, nbk, prof, bscale, false);
         for (uint32_t i = threadIdx.x; i < no; i += kThreads) {
             const uint32_t p = o.logp[i];
             m.t[p] = -m.t[p];
@@ -1808,7 +1175,7 @@ __global__ __launch_bounds__(kThreads) void sq_fmm_kernel(SqWs w, double bscale,
         }
         return;
     }
-    const uint32_t ni = fmm_pass<true>(m, m.sI, nb, L, nbk, prof, bscale, pub != 0, cw ? cs + kCwSt : nullptr);
+    const uint32_t ni = fmm_pass<true>(m, m.sI, nb, L, nbk, prof, bscale, pub != 0);
     {
         uint64_t last = 0;
         publish_prog(m, ni, last, true);  // (fmm_pass ended on a barrier after its last stores)
@@ -3483,17 +2850,17 @@ __global__ __launch_bounds__(256) void sq_unpack_kernel(SqWs w, float *__restric
 }
 
 
-// Helper streams and events of the grouped sequential fill (seq_groups), one
-// set per device, created on that device on first use.  A call uses the set
-// of its stream's device (hipStreamGetDevice), so its group launches always
-// run on the device that owns the workspace, image and output pointers,
-// whichever device is current.
+// The helper stream and events of the pipelined sequential fill (its
+// RECORD / colour rounds beside the marches), one set per device, created on
+// that device on first use.  A call uses the set of its stream's device
+// (hipStreamGetDevice), so its rounds always run on the device that owns the
+// workspace, image and output pointers, whichever device is current.
 struct SeqHelpers {
     std::mutex mu;
     int device = -1;  // created for this device (-1: not yet)
     bool ok = false;
-    hipStream_t stream[3] = {nullptr, nullptr, nullptr};
-    hipEvent_t fork = nullptr, join[3] = {nullptr, nullptr, nullptr};
+    hipStream_t stream[1] = {nullptr};
+    hipEvent_t fork = nullptr, join[1] = {nullptr};
 };
 constexpr int kMaxSeqDevices = 64;
 
@@ -3518,7 +2885,7 @@ SeqHelpers *seq_helpers(int dev) {
         int prev = -1;
         bool ok = hipGetDevice(&prev) == hipSuccess && (prev == dev || hipSetDevice(dev) == hipSuccess);
         ok = ok && hipEventCreateWithFlags(&x.fork, hipEventDisableTiming) == hipSuccess;
-        for (int k = 0; k < 3 && ok; ++k)
+        for (int k = 0; k < 1 && ok; ++k)
             ok = hipStreamCreateWithFlags(&x.stream[k], hipStreamNonBlocking) == hipSuccess &&
                  hipEventCreateWithFlags(&x.join[k], hipEventDisableTiming) == hipSuccess;
         if (prev >= 0 && prev != dev) (void)hipSetDevice(prev);
@@ -3528,12 +2895,6 @@ SeqHelpers *seq_helpers(int dev) {
     return &x;
 }
 
-// Groups of the batch (OFD_SEQ_GROUPS, default 1; at most 4): only when
-// every group of ceil(B / groups) images fits its own 256-aligned slice of
-// the workspace in one chunk, and each group holds at least 2 images.
-#ifndef OFD_SEQ_GROUPS_DEFAULT
-#define OFD_SEQ_GROUPS_DEFAULT 1
-#endif
 // Pipelined radius-3 fill (ofd_inpaint_seq_set_pipeline): record / colour
 // rounds on a helper stream beside the marches.  -1 = not set (OFD_SEQ_PIPE
 // rounds, default 12; OFD_SEQ_PIPE_US per round, default 2000: 12 x 2 ms
@@ -3562,23 +2923,12 @@ int pipe_us_setting() {
     }
     return g_pipe_us;
 }
-// Chip-wide early buckets (sq_cw_*): up to this many buckets of each march
-// run as chunk launches over all marches before sq_fmm_kernel takes over;
-// 0 = off.  OFD_SEQ_CW, else 0: measured slower (64 x 768 x 1024: fill 46.9
-// vs 43.1 ms; the early buckets of all 128 marches take ~12 ms chip-wide,
-// against ~15 ms for the slowest march on its own workgroup, while the 128
-// workgroups already run side by side -- DESIGN.md section 5).
-#ifndef OFD_SEQ_CW_DEFAULT
-#define OFD_SEQ_CW_DEFAULT 0
-#endif
-int g_cw_buckets = -1;
-uint32_t g_cw_min = kCwMinDefault;
 // the colour pass: 1 = levels-free (sq_colour3df_kernel), 0 = level-synchronous
 // COLOUR3; ofd_inpaint_seq_set_colour, default OFD_SEQ_DF (else 1)
 int g_df_colour = [] {
     const char *e = getenv("OFD_SEQ_DF");
     return e ? (atoi(e) != 0 ? 1 : 0) : 1;
-}();  // ofd_inpaint_seq_set_chipwide (tests: 0 keeps small marches chip-wide)
+}();
 // Workgroups per image of the levels-free colour pass (kMW: 256 threads
 // each, sharing the image's queues; 1 = one 1024-thread workgroup, the
 // single-CU pass).  ofd_inpaint_seq_set_multi, default OFD_SEQ_MW (else
@@ -3592,39 +2942,10 @@ int g_seq_multi = [] {
     return v < 1 ? 1 : (v > 16 ? 16 : v);
 }();
 int g_mw_force = 0;  // ofd_inpaint_seq_set_multi(k, 1): also below kPipeMinPixels (tests)
-int cw_buckets_setting() {
-    if (g_cw_buckets < 0) {
-        const char *e = getenv("OFD_SEQ_CW");
-        const int v = e ? atoi(e) : OFD_SEQ_CW_DEFAULT;
-        g_cw_buckets = v < 0 ? 0 : (v > 64 ? 64 : v);
-    }
-    return g_cw_buckets;
-}
-
 // images below this many pixels: marches too short to overlap (unless a
 // test forces the pipeline with ofd_inpaint_seq_set_pipeline(rounds, us, 1))
 int g_pipe_force = 0;
 constexpr int64_t kPipeMinPixels = int64_t(1) << 18;
-
-int g_seq_groups = -1;  // ofd_inpaint_seq_set_groups; -1 = not set (OFD_SEQ_GROUPS, else the default)
-int seq_groups_setting() {
-    if (g_seq_groups < 0) {
-        const char *e = getenv("OFD_SEQ_GROUPS");
-        const int v = e ? atoi(e) : OFD_SEQ_GROUPS_DEFAULT;
-        g_seq_groups = v < 1 ? 1 : (v > 4 ? 4 : v);
-    }
-    return g_seq_groups;
-}
-
-int seq_groups(int64_t B, int64_t G, size_t pi, size_t avail) {
-    int ng = seq_groups_setting();
-    while (ng > 1) {
-        const int64_t per = (B + ng - 1) / ng;
-        if (per >= 2 && G >= B && size_t(ng) * align256(size_t(per) * pi) <= avail) break;
-        --ng;
-    }
-    return ng;
-}
 
 }  // namespace
 
@@ -3661,13 +2982,6 @@ int ofd_inpaint_seq_set_multi(int workgroups, int force) {
     return prev;
 }
 
-int ofd_inpaint_seq_set_chipwide(int buckets, int min_pending) {
-    const int prev = cw_buckets_setting();
-    if (buckets >= 0) g_cw_buckets = buckets > 64 ? 64 : buckets;
-    if (min_pending >= 0) g_cw_min = uint32_t(min_pending);
-    return prev;
-}
-
 int ofd_inpaint_seq_set_pipeline(int rounds, int round_us, int force) {
     const int prev = pipe_rounds_setting();
     (void)pipe_us_setting();
@@ -3678,12 +2992,6 @@ int ofd_inpaint_seq_set_pipeline(int rounds, int round_us, int force) {
     }
     if (round_us >= 1) g_pipe_us = round_us;
     if (force >= 0) g_pipe_force = force ? 1 : 0;
-    return prev;
-}
-
-int ofd_inpaint_seq_set_groups(int groups) {
-    const int prev = seq_groups_setting();
-    if (groups >= 1) g_seq_groups = groups > 4 ? 4 : groups;
     return prev;
 }
 
@@ -3733,7 +3041,6 @@ int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float 
             khz = 100000;  // the MI355X's 100 MHz constant clock
         pipe_ticks = uint64_t(pipe_us_setting()) * uint64_t(khz) / 1000u;
     }
-    const int cwk = cw_buckets_setting();
     const bool df_colour = g_df_colour != 0;
     // kMW: each workgroup's overflow slice of fr2 (en / mw entries) must hold
     // its LDS queue's worst case: kDfQ + OFD_MW_CAP + 8 waves x 480 new holes
@@ -3754,31 +3061,6 @@ int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float 
         hipLaunchKernelGGL(sq_band_scan_kernel, dim3(unsigned(nb)), dim3(kThreads), 0, s, w);
         hipLaunchKernelGGL(sq_band_write_kernel, dim3(unsigned((w.eh + 3) / 4), unsigned(nb)), dim3(256), 0, s, w);
         const dim3 rgrid(unsigned((w.ew + 63) / 64), unsigned((w.eh + kRecTH - 1) / kRecTH), unsigned(nb));
-        // the marches' large first buckets, chip-wide (both marches of every image at once)
-        const int segs = int(2 * nb);
-        const int cwe = segs <= kCwMaxSegs ? cwk : 0;
-        if (cwe > 0) {
-            const dim3 cg(kCwGrid), ct(kCwT);
-            for (int k = 0; k < cwe; ++k) {
-                hipLaunchKernelGGL(sq_cw_begin_kernel, dim3(unsigned(segs)), dim3(64), 0, s, w, k, g_cw_min);
-                if (k > 0) {
-                    hipLaunchKernelGGL(sq_cw_select_kernel, cg, ct, 0, s, w, segs, k, bscale);
-                    hipLaunchKernelGGL(sq_cw_scan_kernel, dim3(unsigned(segs)), ct, 0, s, w, 0);
-                    hipLaunchKernelGGL(sq_cw_write_kernel, cg, ct, 0, s, w, segs, k, bscale);
-                    hipLaunchKernelGGL(sq_cw_runsort_kernel, cg, ct, 0, s, w, segs);
-                    for (int p = 0; (int64_t(kCwCh) << p) < w.en; ++p)
-                        hipLaunchKernelGGL(sq_cw_merge_kernel, cg, ct, 0, s, w, segs, p);
-                }
-                hipLaunchKernelGGL(sq_cw_claim_kernel, cg, ct, 0, s, w, segs);
-                hipLaunchKernelGGL(sq_cw_pcount_kernel, cg, ct, 0, s, w, segs);
-                hipLaunchKernelGGL(sq_cw_scan_kernel, dim3(unsigned(segs)), ct, 0, s, w, 1);
-                hipLaunchKernelGGL(sq_cw_push_kernel, cg, ct, 0, s, w, segs);
-                for (int it = 0; it < kCwSweeps; ++it) hipLaunchKernelGGL(sq_cw_sweep_kernel, cg, ct, 0, s, w, segs, it);
-                hipLaunchKernelGGL(sq_cw_sweep_rest_kernel, dim3(unsigned(segs)), ct, 0, s, w);
-                hipLaunchKernelGGL(sq_cw_log_kernel, cg, ct, 0, s, w, segs);
-                hipLaunchKernelGGL(sq_cw_end_kernel, dim3(unsigned(segs)), dim3(64), 0, s, w, k);
-            }
-        }
         // kMW: the shared queues' granules are tagged by slot, which restarts
         // at 0 every fill -- clear the previous fill's tags
         if (rec3 && mw > 1) (void)hipMemsetAsync(w.cy, 0, size_t(nb) * size_t(w.en) * 8, s);
@@ -3810,12 +3092,12 @@ int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float 
             std::lock_guard<std::mutex> lk(hp->mu);
             (void)hipEventRecord(hp->fork, s);  // after BAND: the helper may start reading
             (void)hipStreamWaitEvent(hp->stream[0], hp->fork, 0);
-            hipLaunchKernelGGL(sq_fmm_kernel, dim3(unsigned(nb), 2u), dim3(kThreads), 0, s, w, bscale, 1, cwe);
+            hipLaunchKernelGGL(sq_fmm_kernel, dim3(unsigned(nb), 2u), dim3(kThreads), 0, s, w, bscale, 1);
             for (int e = 0; e < rounds; ++e) round(hp->stream[0], e, 0);
             (void)hipEventRecord(hp->join[0], hp->stream[0]);
             (void)hipStreamWaitEvent(s, hp->join[0], 0);
         } else {
-            hipLaunchKernelGGL(sq_fmm_kernel, dim3(unsigned(nb), 2u), dim3(kThreads), 0, s, w, bscale, 0, cwe);
+            hipLaunchKernelGGL(sq_fmm_kernel, dim3(unsigned(nb), 2u), dim3(kThreads), 0, s, w, bscale, 0);
         }
 #ifdef OFD_BUCKET_TRACE
         return;  // probe: keep the record area (the inner march's bucket trace) for the host
@@ -3835,40 +3117,8 @@ int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float 
             hipLaunchKernelGGL(sq_colour_kernel, dim3(unsigned(nb)), dim3(kColThreads), 0, s, w, out, int(C), int(H),
                                int(W), b0, r);
     };
-    // Groups: the batch split over the caller's stream and up to three
-    // helper streams, each group's chunk in its own slice of the workspace.
-    // An image's chain (FMM, then its Kahn levels) is serial and takes one or
-    // two CUs, so a single chunk costs max FMM + max COLOUR over all its
-    // images; groups overlap one group's colour pass with another's march.
-    const int ng = seq_groups(B, G, pi, workspace_bytes - fixed);
-    if (ng <= 1) {
-        const SqWs w = carve(workspace, G, H, W);
-        for (int64_t b0 = 0; b0 < B; b0 += G) run_chunk(w, b0, B - b0 < G ? B - b0 : G, st);
-    } else {
-        rounds = 0;  // the helper streams carry the groups (and their mutex is held below)
-        SeqHelpers *hpp = seq_helpers(stream_device(st));
-        if (!hpp || !hpp->ok) return OFD_FW_EWORKSPACE;
-        SeqHelpers &hp = *hpp;
-        // one caller at a time enqueues on the shared helper streams: each
-        // event's record / wait pair must not interleave with another's
-        std::lock_guard<std::mutex> lk(hp.mu);
-        hipError_t e = hipEventRecord(hp.fork, st);
-        const int64_t per = (B + ng - 1) / ng;
-        const size_t stride = align256(size_t(per) * pi);
-        for (int k = 0; k < ng && e == hipSuccess; ++k) {
-            const int64_t b0 = int64_t(k) * per, nb = std::min<int64_t>(per, B - b0);
-            if (nb <= 0) break;
-            hipStream_t s = k == 0 ? st : hp.stream[k - 1];
-            if (k > 0) e = hipStreamWaitEvent(s, hp.fork, 0);
-            if (e != hipSuccess) break;
-            run_chunk(carve(static_cast<char *>(workspace) + size_t(k) * stride, nb, H, W), b0, nb, s);
-            if (k > 0) {
-                e = hipEventRecord(hp.join[k - 1], s);
-                if (e == hipSuccess) e = hipStreamWaitEvent(st, hp.join[k - 1], 0);
-            }
-        }
-        if (e != hipSuccess) return int(e);
-    }
+    const SqWs w = carve(workspace, G, H, W);
+    for (int64_t b0 = 0; b0 < B; b0 += G) run_chunk(w, b0, B - b0 < G ? B - b0 : G, st);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? OFD_FW_OK : int(e);
 }

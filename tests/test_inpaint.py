@@ -462,73 +462,6 @@ def test_inpaint_sequential_wide_image_half_unit_buckets():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("groups", [2, 4])
-def test_inpaint_sequential_stream_groups(groups):
-    """ofd_inpaint_seq_set_groups: the batch split over the caller's stream and
-    library helper streams (each group in its own workspace slice, forked from
-    and joined back into the caller's stream) gives the one-stream result bit
-    for bit, and the oracle's; the caller's stream sees the whole fill."""
-    from opticalflowfromdepth_amd import _native, forward_warp_flow, ops, synth
-    lib = _native.lib()
-    dev = torch.device("cuda:0")
-    seeds = [12345, 12346, 12377, 12378, 12401, 12402, 12433, 12434]
-    obj, flow, depth = synth.stage_one_batch(seeds, 384, 512, dev)
-    out, valid, coll = forward_warp_flow(obj, flow, depth)
-    rgb = (out[:, 0:3] * valid).contiguous()
-    prev = lib.ofd_inpaint_seq_set_groups(1)
-    try:
-        one = ops.inpaint(rgb, valid, coll, order="sequential")
-        lib.ofd_inpaint_seq_set_groups(groups)
-        side = torch.cuda.Stream()
-        with torch.cuda.stream(side):
-            got = ops.inpaint(rgb, valid, coll, order="sequential")
-            got_host = got.cpu().numpy()  # synchronises the caller's (side) stream only
-    finally:
-        lib.ofd_inpaint_seq_set_groups(prev)
-    assert np.array_equal(got_host, one.cpu().numpy())
-    exp = oracle.inpaint(rgb.cpu().numpy(), valid.cpu().numpy(), coll.cpu().numpy(), 3, layered=False)
-    assert np.array_equal(got_host, exp)
-
-
-@pytest.mark.gpu
-def test_inpaint_sequential_stream_groups_concurrent_callers():
-    """Two host threads fill different batches with stream groups on their own
-    streams at once: the library's helper streams are shared, and each call's
-    fork / join stays its own (results equal the one-stream fills)."""
-    import threading
-    from opticalflowfromdepth_amd import _native, forward_warp_flow, ops, synth
-    lib = _native.lib()
-    dev = torch.device("cuda:0")
-    batches = []
-    for seeds in ([12345, 12346, 12377, 12378], [12401, 12402, 12433, 12434]):
-        obj, flow, depth = synth.stage_one_batch(seeds, 256, 320, dev)
-        out, valid, coll = forward_warp_flow(obj, flow, depth)
-        batches.append(((out[:, 0:3] * valid).contiguous(), valid, coll))
-    prev = lib.ofd_inpaint_seq_set_groups(1)
-    try:
-        ref = [ops.inpaint(*x, order="sequential").cpu().numpy() for x in batches]
-        lib.ofd_inpaint_seq_set_groups(2)
-        got = [None, None]
-
-        def run(i):
-            s = torch.cuda.Stream()
-            with torch.cuda.stream(s):
-                for _ in range(3):
-                    r = ops.inpaint(*batches[i], order="sequential")
-                got[i] = r.cpu().numpy()
-
-        th = [threading.Thread(target=run, args=(i,)) for i in range(2)]
-        for t in th:
-            t.start()
-        for t in th:
-            t.join()
-    finally:
-        lib.ofd_inpaint_seq_set_groups(prev)
-    for i in range(2):
-        assert np.array_equal(got[i], ref[i])
-
-
-@pytest.mark.gpu
 def test_inpaint_sequential_helpers_follow_the_stream_device(cuda_device):
     """The grouped fill's helper streams are kept per device and chosen by the
     caller's stream's device: a call on a stream of device d
@@ -574,59 +507,6 @@ def test_inpaint_sequential_pipelined_rounds_bit_exact(case, seq_pipeline):
     exp = oracle.inpaint(img, v, c, r, layered=False)
     bad = np.argwhere(got != exp)
     assert bad.size == 0, f"{name}: {len(bad)} differing values, first {bad[:5].tolist()}"
-
-
-@pytest.fixture
-def seq_chipwide():
-    """Sets the chip-wide early buckets for one test (ofd_inpaint_seq_set_chipwide)
-    and restores the defaults afterwards."""
-    from opticalflowfromdepth_amd import _native
-    lib = _native.lib()
-    prev = lib.ofd_inpaint_seq_set_chipwide(-1, -1)
-
-    def set_(buckets, min_pending):
-        lib.ofd_inpaint_seq_set_chipwide(buckets, min_pending)
-    yield set_
-    lib.ofd_inpaint_seq_set_chipwide(prev, 16384)
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("buckets", [8, 3, 64])
-@pytest.mark.parametrize("case", _gpu_cases() + _seq_extra_cases(), ids=lambda c: c[0])
-def test_inpaint_sequential_chipwide_buckets_bit_exact(case, buckets, seq_chipwide):
-    """The marches' first buckets as chip-wide launches (opt-in; kept chip-wide
-    down to no pending entries: 3 or 8 buckets then the workgroup, or all of
-    them): cv2's order bit for bit."""
-    from opticalflowfromdepth_amd import ops
-    name, img, v, c, r = case
-    dev = torch.device("cuda:0")
-    seq_chipwide(buckets, 0)
-    got = ops.inpaint(torch.from_numpy(img).to(dev), torch.from_numpy(v).to(dev), torch.from_numpy(c).to(dev),
-                      radius=r, order="sequential").cpu().numpy()
-    exp = oracle.inpaint(img, v, c, r, layered=False)
-    bad = np.argwhere(got != exp)
-    assert bad.size == 0, f"{name}: {len(bad)} differing values, first {bad[:5].tolist()}"
-    from opticalflowfromdepth_amd import _native
-    assert _native.lib().ofd_inpaint_faults(1) == 0
-
-
-@pytest.mark.gpu
-def test_inpaint_sequential_chipwide_buckets_on_warped_images(seq_chipwide):
-    """Warped 768x1024 images (8 at once): band- and ring-sized buckets of
-    ~100 k pops, so the chip-wide path's merge passes and multi-chunk scans
-    run; the same bits as the oracle's cv2 order."""
-    from opticalflowfromdepth_amd import forward_warp_flow, ops, synth
-    dev = torch.device("cuda:0")
-    seeds = [12345, 12346, 12377, 12378, 12401, 12402, 12433, 12434]
-    obj, flow, depth = synth.stage_one_batch(seeds, 768, 1024, dev)
-    out, valid, coll = forward_warp_flow(obj, flow, depth)
-    rgb = (out[:, 0:3] * valid).contiguous()
-    seq_chipwide(8, 16384)
-    got = ops.inpaint(rgb, valid, coll, order="sequential").cpu().numpy()
-    exp = oracle.inpaint(rgb.cpu().numpy(), valid.cpu().numpy(), coll.cpu().numpy(), 3, layered=False)
-    assert np.array_equal(got, exp)
-    from opticalflowfromdepth_amd import _native
-    assert _native.lib().ofd_inpaint_faults(1) == 0
 
 
 @pytest.fixture

@@ -88,9 +88,10 @@ def test_disparity_rows_switch():
 
 
 def test_schedule_setters_are_host_state():
-    """The persistent-SPLAT threshold and the sequential fill's stream groups
-    are process-wide host settings: a negative value queries, a valid one
-    sets and returns the previous (groups clamp to 1..4)."""
+    """The persistent-SPLAT threshold, the packed / short-tile switches and the
+    sequential fill's pipeline, colour pass and workgroups per image are
+    process-wide host settings: a negative (or out-of-range) value queries, a
+    valid one sets and returns the previous."""
     from opticalflowfromdepth_amd import _native
     lib = _native.lib()
     cur = lib.ofd_fw_set_persist_min(-1)
@@ -120,24 +121,12 @@ def test_schedule_setters_are_host_state():
     assert lib.ofd_inpaint_seq_set_pipeline(999, -1, -1) == 5  # clamps to 256
     assert lib.ofd_inpaint_seq_set_pipeline(-1, -1, -1) == 256
     lib.ofd_inpaint_seq_set_pipeline(pr, 0, 0)
-    cw = lib.ofd_inpaint_seq_set_chipwide(-1, -1)
-    assert 0 <= cw <= 64
-    assert lib.ofd_inpaint_seq_set_chipwide(3, 0) == cw
-    assert lib.ofd_inpaint_seq_set_chipwide(999, -1) == 3  # clamps to 64
-    assert lib.ofd_inpaint_seq_set_chipwide(-1, -1) == 64
-    lib.ofd_inpaint_seq_set_chipwide(cw, 16384)
     cm = lib.ofd_inpaint_seq_set_colour(-1)
     assert cm in (0, 1)
     assert lib.ofd_inpaint_seq_set_colour(1 - cm) == cm
     assert lib.ofd_inpaint_seq_set_colour(5) == 1 - cm  # any nonzero: levels-free
     assert lib.ofd_inpaint_seq_set_colour(-1) == 1
     lib.ofd_inpaint_seq_set_colour(cm)
-    g = lib.ofd_inpaint_seq_set_groups(-1)
-    assert 1 <= g <= 4
-    assert lib.ofd_inpaint_seq_set_groups(9) == g
-    assert lib.ofd_inpaint_seq_set_groups(2) == 4
-    assert lib.ofd_inpaint_seq_set_groups(-1) == 2
-    lib.ofd_inpaint_seq_set_groups(g)
 
 
 def test_argument_errors_without_gpu():
