@@ -138,6 +138,8 @@ constexpr int kPT0 = 36;       // image 0: the pacing clock origin (2 words)
 // round with work, rounds with work (pacing line)
 constexpr int kPTFmm = 8, kPTOut = 10, kPTIn = 12, kPTc0 = 40, kPTc1 = 42, kPCRounds = 44;
 constexpr int kPCarry = 46;    // frontier entries a COLOUR3 round left in cy for the next
+constexpr int kPAllDone = 60;   // image 0: every march of the chunk was done at this round's snapshot (PACE)
+constexpr int kPB0Out = 4, kPB0In = 5;  // pushes of bucket 0 (the band) of the outer / inner march (BAND PUSH)
 __device__ __forceinline__ void put64(uint32_t *p, uint64_t v) {
     p[0] = uint32_t(v);
     p[1] = uint32_t(v >> 32);
@@ -468,6 +470,151 @@ __global__ __launch_bounds__(256) void sq_band_write_kernel(SqWs w) {
             reinterpret_cast<float *>(m.olog + m.en)[s] = 0.f;
         }
         off += __popcll(bal);
+    }
+}
+
+// ---------------------------------------------------------------- BAND PUSH
+// Bucket 0 of both marches -- its claims, push numbering, stamps and log
+// entries -- as raster passes over all images before FMM (one wave per
+// padded row), instead of claim atomics and dependent log loads inside the
+// one-workgroup marches (~1.6 ms of each march on the deep images).  Bucket 0
+// pops the band, whose log is raster order, so a pixel's claimant -- its
+// neighbour of least pop rank -- is its first band neighbour in raster order
+// (up, left, right, down), and band pixel b pushes its INSIDE neighbour n in
+// direction q exactly when no band neighbour of n precedes b:
+//   q = 0 (n above b):    none of n's up, left, right neighbours is band;
+//   q = 1 (n left of b):  neither n's up nor n's left neighbour is band;
+//   q = 2 (n below b):    always (b is n's first neighbour);
+//   q = 3 (n right of b): n's up neighbour is not band.
+// Pushes are numbered in (rank, direction) order: the pushes of each padded
+// row's band pixels (COUNT), an exclusive scan over the rows (SCAN), then
+// each band pixel's pushes at its row's offset + the pushes of the row's
+// earlier band pixels, in direction order (WRITE).  A pixel is band iff its
+// distance is 0 (INIT).  The distances are left to the march's sweeps; the
+// claim words (own) are not needed: a pushed pixel is never claimed again.
+// blockIdx.z: 0 = the outer march (ring stamps sO, log olog), 1 = the inner
+// march (hole stamps sI, log logp).
+constexpr int kBpU = 2;  // 64-pixel chunks of a row per load round
+__device__ __forceinline__ void band_push_bits(const float *t, const uint32_t *st, int i, int j0, int lane, int ew,
+                                               unsigned (&c)[kBpU]) {
+    float tb[kBpU], tu2[kBpU], tul[kBpU], tur[kBpU], tl2[kBpU];
+    uint32_t su[kBpU], sl[kBpU], sd[kBpU], sr[kBpU];
+    const int64_t r0 = int64_t(i) * ew, rm1 = r0 - ew, rm2 = int64_t(max(i - 2, 0)) * ew;
+    // every load first, at clamped positions (a clamped position is frame,
+    // never band; the stamps are read only for band pixels, which are interior)
+#pragma unroll
+    for (int u = 0; u < kBpU; ++u) {
+        const int j = min(j0 + 64 * u + lane, ew - 1);
+        tb[u] = t[r0 + j];
+        tu2[u] = t[rm2 + j];
+        tul[u] = t[rm1 + max(j - 1, 0)];
+        tur[u] = t[rm1 + min(j + 1, ew - 1)];
+        tl2[u] = t[r0 + max(j - 2, 0)];
+        su[u] = st[rm1 + j];
+        sl[u] = st[r0 + j - 1];
+        sd[u] = st[r0 + ew + j];
+        sr[u] = st[r0 + j + 1];
+    }
+#pragma unroll
+    for (int u = 0; u < kBpU; ++u) {
+        const bool band = j0 + 64 * u + lane < ew && tb[u] == 0.f;
+        const bool bu2 = i >= 2 && tu2[u] == 0.f, bul = tul[u] == 0.f, bur = tur[u] == 0.f, bl2 = tl2[u] == 0.f;
+        unsigned v = 0;
+        v |= (su[u] == INF && !bu2 && !bul && !bur) ? 1u : 0u;
+        v |= (sl[u] == INF && !bul && !bl2) ? 2u : 0u;
+        v |= sd[u] == INF ? 4u : 0u;
+        v |= (sr[u] == INF && !bur) ? 8u : 0u;
+        c[u] = band ? v : 0u;
+    }
+}
+
+// wave-wide exclusive prefix and total of a 0..7 count, by bit planes
+__device__ __forceinline__ uint32_t wave_scan_small(unsigned v, uint32_t &tot) {
+    const uint64_t below = (uint64_t(1) << (threadIdx.x & 63)) - 1;
+    uint32_t ex = 0;
+    tot = 0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const uint64_t bal = __ballot((v >> k) & 1u);
+        ex += uint32_t(__popcll(bal & below)) << k;
+        tot += uint32_t(__popcll(bal)) << k;
+    }
+    return ex;
+}
+
+__device__ __forceinline__ uint32_t *band_push_rows(const Img &m, bool inner) {
+    return inner ? reinterpret_cast<uint32_t *>(m.k0) : m.olog + 2 * m.en;  // the march's sort buffer: free until FMM
+}
+
+__global__ __launch_bounds__(256) void sq_band_push_count_kernel(SqWs w) {
+    const int lane = threadIdx.x & 63, i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const Img m = image(w, blockIdx.y);
+    if (i >= m.eh) return;
+    const bool inner = blockIdx.z != 0;
+    const uint32_t *st = inner ? m.sI : m.sO;
+    uint32_t row = 0;
+    if (i >= 1 && i < m.eh - 1)
+        for (int j0 = 0; j0 < m.ew; j0 += 64 * kBpU) {
+            unsigned c[kBpU];
+            band_push_bits(m.t, st, i, j0, lane, m.ew, c);
+#pragma unroll
+            for (int u = 0; u < kBpU; ++u) {
+                uint32_t tot;
+                (void)wave_scan_small(unsigned(__popc(c[u])), tot);
+                row += tot;
+            }
+        }
+    if (lane == 0) band_push_rows(m, inner)[i] = row;
+}
+
+__global__ __launch_bounds__(kThreads) void sq_band_push_scan_kernel(SqWs w) {
+    __shared__ uint32_t scr[40];
+    const Img m = image(w, blockIdx.x);
+    const bool inner = blockIdx.y != 0;
+    uint32_t *rowp = band_push_rows(m, inner);
+    uint32_t carry = 0;
+    for (int i0 = 0; i0 < m.eh; i0 += kThreads) {
+        const int i = i0 + threadIdx.x;
+        const uint32_t v = i < m.eh ? rowp[i] : 0u;
+        uint32_t tot;
+        const uint32_t ex = block_scan(v, tot, scr);
+        if (i < m.eh) rowp[i] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) m.pipe[inner ? kPB0In : kPB0Out] = carry;
+}
+
+__global__ __launch_bounds__(256) void sq_band_push_write_kernel(SqWs w) {
+    const int lane = threadIdx.x & 63, i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const Img m = image(w, blockIdx.y);
+    if (i < 1 || i >= m.eh - 1) return;
+    const bool inner = blockIdx.z != 0;
+    uint32_t *st = inner ? m.sI : m.sO, *logp = inner ? m.logp : m.olog;
+    const int ew = m.ew;
+    const int64_t off[4] = {-int64_t(ew), -1, int64_t(ew), 1};
+    // (a chunk's stamp stores cannot change a later chunk's bits: only a
+    // pixel's claimant pushes it, and for its other band neighbours the rule
+    // is false by the band flags alone)
+    uint32_t base = m.meta[0] + band_push_rows(m, inner)[i];
+    for (int j0 = 0; j0 < ew; j0 += 64 * kBpU) {
+        unsigned c[kBpU];
+        band_push_bits(m.t, st, i, j0, lane, ew, c);
+#pragma unroll
+        for (int u = 0; u < kBpU; ++u) {
+            uint32_t tot;
+            uint32_t s = base + wave_scan_small(unsigned(__popc(c[u])), tot);
+            if (c[u]) {
+                const int64_t p = int64_t(i) * ew + j0 + 64 * u + lane;
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (c[u] & (1u << q)) {
+                        st[p + off[q]] = s;
+                        logp[s] = uint32_t(p + off[q]);
+                        ++s;
+                    }
+            }
+            base += tot;
+        }
     }
 }
 
@@ -882,7 +1029,10 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
 #ifdef OFD_BUCKET_TRACE
         const uint64_t tb2 = __builtin_amdgcn_s_memtime();
 #endif
+        // the band's claims and pushes are already made (sq_band_push_*_kernel)
+        uint32_t npush = band ? m.pipe[kInner ? kPB0In : kPB0Out] : 0u;
         // pops in order: claim the INSIDE neighbours (first claimant = pusher)
+        if (!band)
         for (uint32_t r0 = tid; r0 < n; r0 += kFB * kThreads) {  // 4 pops per thread: one round per load step
             int64_t a[kFB];
             uint32_t sv[kFB][4];
@@ -909,7 +1059,7 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
         const uint64_t tb3 = __builtin_amdgcn_s_memtime();
 #endif
         // pushes numbered in (rank, direction) order
-        uint32_t npush = 0;
+        if (!band)
         for (uint32_t b = 0; b < n; b += kFB * kThreads) {  // kFB slices of kThreads ranks, loads first
             int64_t a[kFB];
             uint32_t sv[kFB][4], ov[kFB][4];
@@ -952,6 +1102,7 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
         SQ_ACC(pb + 3, f3, f4);
 #ifdef OFD_BUCKET_TRACE
         const uint64_t tb4 = __builtin_amdgcn_s_memtime();
+        uint32_t nsw = 0;  // probe: sweeps of this bucket
 #endif
         // distances: sweep to the fixed point (acyclic in push order: at most
         // npush + 1 sweeps; the cap only guards against a broken invariant).
@@ -1014,6 +1165,9 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
 #ifdef OFD_SQ_PROF
                 if (tid == 0) prof[pb + 6] += 1;
 #endif
+#ifdef OFD_BUCKET_TRACE
+                nsw = it + 1;
+#endif
                 if (!c) break;
             }
             for (uint32_t i = tid; i < npush; i += kThreads) {
@@ -1038,7 +1192,7 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
                 tr[7] = uint32_t((tb4 - tb3) >> 4);
                 tr[1] = n;
                 tr[2] = npush;
-                tr[3] = k;
+                tr[3] = k | (nsw << 16);
                 m.rec[(kInner ? 8 : 20) * m.en + 4 * m.en] = nbuckets;
             }
 #endif
@@ -1097,6 +1251,9 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
                 uint32_t *tmp = wa;
                 wa = wb;
                 wb = tmp;
+#ifdef OFD_BUCKET_TRACE
+                nsw = it + 1;
+#endif
                 if (nw == 0) break;
             }
         }
@@ -1118,7 +1275,7 @@ __device__ uint32_t fmm_pass(const Img &m, uint32_t *st, uint32_t nb, FmmLds &L,
             tr[7] = uint32_t((tb4 - tb3) >> 4);
             tr[1] = n;
             tr[2] = npush;
-            tr[3] = k;
+            tr[3] = k | (nsw << 16);
             m.rec[(kInner ? 8 : 20) * m.en + 4 * m.en] = nbuckets;
         }
 #endif
@@ -1871,7 +2028,7 @@ __global__ __launch_bounds__(1024) void sq_colour3_kernel(SqWs w, int C, int H, 
             ga[x] = en;
     }
     const uint64_t deadline =
-        fin ? ~uint64_t(0)
+        (fin || w.pipe[kPAllDone]) ? ~uint64_t(0)
             : (uint64_t(w.pipe[kPT0]) | (uint64_t(w.pipe[kPT0 + 1]) << 32)) + round_ticks * uint64_t(e + 2);
     if (tid == 0) L.nnext[0] = 0u;
     sync_all();  // (fr3's entries are read back by other waves)
@@ -2222,7 +2379,7 @@ __global__ __launch_bounds__(kThr) void sq_colour3df_kernel(SqWs w, int C, int H
     }
     sync_all();
     const uint64_t deadline =
-        fin ? ~uint64_t(0)
+        (fin || w.pipe[kPAllDone]) ? ~uint64_t(0)
             : (uint64_t(w.pipe[kPT0]) | (uint64_t(w.pipe[kPT0 + 1]) << 32)) + round_ticks * uint64_t(e + 2);
     const uint64_t tstart = wall_clock64();
     const int nch = 3 * C;
@@ -2827,8 +2984,14 @@ __global__ __launch_bounds__(256) void sq_pace_kernel(SqWs w, int nimg, int e, i
         }
         __syncthreads();
     }
+    // snapshot; and whether every march is done (each image's inner march
+    // done before its progress is read, so hi is then its whole log): this
+    // round then records every hole, and its colour pass runs to the end
+    // (no deadline, no further round boundaries)
+    int done = 1;
     for (int b = threadIdx.x; b < nimg; b += 256) {
         uint32_t *pp = w.pipe + int64_t(b) * kPipe;
+        const uint32_t id = __hip_atomic_load(pp + kPInDone, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t od = __hip_atomic_load(pp + kPOutDone, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t prog = __hip_atomic_load(pp + kPProg, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t lo = pp[kPRecDone];
@@ -2836,7 +2999,13 @@ __global__ __launch_bounds__(256) void sq_pace_kernel(SqWs w, int nimg, int e, i
         pp[kPLo] = lo;
         pp[kPHi] = hi;
         pp[kPRecDone] = hi;
+        if (id == 0u || od == 0u) done = 0;
     }
+    done = __syncthreads_and(done);
+#ifndef OFD_SEQ_ALLDONE  // probe builds: 0 keeps every helper round's deadline (A/B)
+#define OFD_SEQ_ALLDONE 1
+#endif
+    if (threadIdx.x == 0) w.pipe[kPAllDone] = (fin || (OFD_SEQ_ALLDONE && done)) ? 1u : 0u;
 }
 
 // The record path's result: every pixel's colours from the shadow image
@@ -3060,6 +3229,11 @@ int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float 
             hipLaunchKernelGGL(sq_init_kernel, dim3(unsigned((w.eh + 3) / 4), unsigned(nb)), dim3(256), 0, s, w, r);
         hipLaunchKernelGGL(sq_band_scan_kernel, dim3(unsigned(nb)), dim3(kThreads), 0, s, w);
         hipLaunchKernelGGL(sq_band_write_kernel, dim3(unsigned((w.eh + 3) / 4), unsigned(nb)), dim3(256), 0, s, w);
+        hipLaunchKernelGGL(sq_band_push_count_kernel, dim3(unsigned((w.eh + 3) / 4), unsigned(nb), 2u), dim3(256), 0, s,
+                           w);
+        hipLaunchKernelGGL(sq_band_push_scan_kernel, dim3(unsigned(nb), 2u), dim3(kThreads), 0, s, w);
+        hipLaunchKernelGGL(sq_band_push_write_kernel, dim3(unsigned((w.eh + 3) / 4), unsigned(nb), 2u), dim3(256), 0, s,
+                           w);
         const dim3 rgrid(unsigned((w.ew + 63) / 64), unsigned((w.eh + kRecTH - 1) / kRecTH), unsigned(nb));
         // kMW: the shared queues' granules are tagged by slot, which restarts
         // at 0 every fill -- clear the previous fill's tags

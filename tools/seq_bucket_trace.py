@@ -62,3 +62,23 @@ for march, off in (("inner", 8), ("outer", 20)):
           g_, so, cl, pu = (ph[sel, c].sum() / 1e3 for c in range(4))
           print(f"  {name} buckets: gather {g_:.2f}, sort {so:.2f}, claim {cl:.2f}, push {pu:.2f}, "
                 f"distances+log {dur[sel].sum() / 1e3 - g_ - so - cl - pu:.2f} ms")
+
+# Per-bucket detail of chosen images (OFD_TRACE_IMAGES="37,54"): time, keys,
+# pushes, sweeps and the phase split of every bucket above 2048 keys.
+for bl in [int(x) for x in os.environ.get("OFD_TRACE_IMAGES", "").split(",") if x]:
+  for march, off in (("inner", 8), ("outer", 20)):
+    base = rec0 + bl * en * 160
+    q = (off * en + 4 * en) * 4
+    nb = int(ws[base + q: base + q + 4].view(torch.int32).item())
+    tr = ws[base + off * en * 4: base + off * en * 4 + nb * 32].view(torch.int32).cpu().numpy().reshape(nb, 8)
+    tr = tr.astype(np.int64) & 0xFFFFFFFF
+    dur = tr[:, 0] * 16 / 2.4e3
+    sw = tr[:, 3] >> 16
+    print(f"image {bl} {march}: {nb} buckets, {dur.sum() / 1e3:.2f} ms, sweeps {int(sw.sum())}, "
+          f"keys {int(tr[:, 1].sum())}, pushes {int(tr[:, 2].sum())}")
+    for r in range(nb):
+        if tr[r, 1] > 2048 or r < 3:
+            ph = tr[r, 4:8] * 16 / 2.4e3
+            print(f"   k {int(tr[r, 3] & 0xFFFF)}: {dur[r]:.0f} us keys {int(tr[r, 1])} pushes {int(tr[r, 2])} "
+                  f"sweeps {int(sw[r])} gather/sort/claim/push {[round(float(x)) for x in ph]} "
+                  f"dist+log {dur[r] - ph.sum():.0f}")
