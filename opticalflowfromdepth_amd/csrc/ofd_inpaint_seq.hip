@@ -494,38 +494,49 @@ __global__ __launch_bounds__(256) void sq_band_write_kernel(SqWs w) {
 // claim words (own) are not needed: a pushed pixel is never claimed again.
 // blockIdx.z: 0 = the outer march (ring stamps sO, log olog), 1 = the inner
 // march (hole stamps sI, log logp).
-constexpr int kBpU = 2;  // 64-pixel chunks of a row per load round
-__device__ __forceinline__ void band_push_bits(const float *t, const uint32_t *st, int i, int j0, int lane, int ew,
-                                               unsigned (&c)[kBpU]) {
-    float tb[kBpU], tu2[kBpU], tul[kBpU], tur[kBpU], tl2[kBpU];
-    uint32_t su[kBpU], sl[kBpU], sd[kBpU], sr[kBpU];
-    const int64_t r0 = int64_t(i) * ew, rm1 = r0 - ew, rm2 = int64_t(max(i - 2, 0)) * ew;
-    // every load first, at clamped positions (a clamped position is frame,
-    // never band; the stamps are read only for band pixels, which are interior)
-#pragma unroll
-    for (int u = 0; u < kBpU; ++u) {
-        const int j = min(j0 + 64 * u + lane, ew - 1);
-        tb[u] = t[r0 + j];
-        tu2[u] = t[rm2 + j];
-        tul[u] = t[rm1 + max(j - 1, 0)];
-        tur[u] = t[rm1 + min(j + 1, ew - 1)];
-        tl2[u] = t[r0 + max(j - 2, 0)];
-        su[u] = st[rm1 + j];
-        sl[u] = st[r0 + j - 1];
-        sd[u] = st[r0 + ew + j];
-        sr[u] = st[r0 + j + 1];
+// Both marches on 64 x 16 tiles of the padded grid (a wave per row of the
+// tile: one 64-pixel row chunk): the tile's band flags with a 2-pixel halo
+// above and to the left and 1 to the right, and both marches' INSIDE flags
+// with a 1-pixel halo, in LDS, so the rule reads LDS.  COUNT stores each row
+// chunk's pushes, SCAN turns them into offsets in raster order (per image and
+// march), WRITE numbers and stores the pushes in direction order.
+constexpr int kBpTW = 64, kBpTH = 16;
+struct BandPushLds {
+    uint8_t band[kBpTH + 2][kBpTW + 3];  // rows i0 - 2 .., columns j0 - 2 .. j0 + 64
+    uint8_t ins[kBpTH + 2][kBpTW + 2];   // rows i0 - 1 .., columns j0 - 1 .. j0 + 64: bit 0 outer INF, bit 1 inner INF
+};
+
+__device__ __forceinline__ void band_push_tile(const Img &m, int i0, int j0, BandPushLds &L) {
+    const int eh = m.eh, ew = m.ew;
+    for (int e = threadIdx.x; e < (kBpTH + 2) * (kBpTW + 3); e += 256) {
+        const int r = e / (kBpTW + 3), c = e - r * (kBpTW + 3);
+        const int y = i0 - 2 + r, x = j0 - 2 + c;
+        L.band[r][c] = (y >= 0 && x >= 0 && y < eh && x < ew && m.t[int64_t(y) * ew + x] == 0.f) ? 1 : 0;
     }
-#pragma unroll
-    for (int u = 0; u < kBpU; ++u) {
-        const bool band = j0 + 64 * u + lane < ew && tb[u] == 0.f;
-        const bool bu2 = i >= 2 && tu2[u] == 0.f, bul = tul[u] == 0.f, bur = tur[u] == 0.f, bl2 = tl2[u] == 0.f;
-        unsigned v = 0;
-        v |= (su[u] == INF && !bu2 && !bul && !bur) ? 1u : 0u;
-        v |= (sl[u] == INF && !bul && !bl2) ? 2u : 0u;
-        v |= sd[u] == INF ? 4u : 0u;
-        v |= (sr[u] == INF && !bur) ? 8u : 0u;
-        c[u] = band ? v : 0u;
+    for (int e = threadIdx.x; e < (kBpTH + 2) * (kBpTW + 2); e += 256) {
+        const int r = e / (kBpTW + 2), c = e - r * (kBpTW + 2);
+        const int y = i0 - 1 + r, x = j0 - 1 + c;
+        uint8_t f = 0;
+        if (y >= 0 && x >= 0 && y < eh && x < ew) {
+            const int64_t q = int64_t(y) * ew + x;
+            f = uint8_t((m.sO[q] == INF ? 1 : 0) | (m.sI[q] == INF ? 2 : 0));
+        }
+        L.ins[r][c] = f;
     }
+}
+
+// push bits of tile pixel (li, lj) for the march whose INSIDE flag is bit mk
+__device__ __forceinline__ unsigned band_push_bits(const BandPushLds &L, int li, int lj, unsigned mk) {
+    const int br = li + 2, bc = lj + 2, ir = li + 1, ic = lj + 1;  // the pixel in band / ins
+    if (!L.band[br][bc]) return 0u;
+    const bool bu2 = L.band[br - 2][bc], bul = L.band[br - 1][bc - 1], bur = L.band[br - 1][bc + 1],
+               bl2 = L.band[br][bc - 2];
+    unsigned v = 0;
+    v |= ((L.ins[ir - 1][ic] & mk) && !bu2 && !bul && !bur) ? 1u : 0u;
+    v |= ((L.ins[ir][ic - 1] & mk) && !bul && !bl2) ? 2u : 0u;
+    v |= (L.ins[ir + 1][ic] & mk) ? 4u : 0u;
+    v |= ((L.ins[ir][ic + 1] & mk) && !bur) ? 8u : 0u;
+    return v;
 }
 
 // wave-wide exclusive prefix and total of a 0..7 count, by bit planes
@@ -542,78 +553,81 @@ __device__ __forceinline__ uint32_t wave_scan_small(unsigned v, uint32_t &tot) {
     return ex;
 }
 
-__device__ __forceinline__ uint32_t *band_push_rows(const Img &m, bool inner) {
-    return inner ? reinterpret_cast<uint32_t *>(m.k0) : m.olog + 2 * m.en;  // the march's sort buffer: free until FMM
+// the per-chunk counts / offsets (eh x nch words, a chunk = 64 columns of a
+// row): the march's sort buffer, free until FMM
+__device__ __forceinline__ uint32_t *band_push_chunks(const Img &m, bool inner) {
+    return inner ? reinterpret_cast<uint32_t *>(m.k0) : m.olog + 2 * m.en;
 }
 
+// grid: (ceil(ew / 64), ceil(eh / 16), images)
 __global__ __launch_bounds__(256) void sq_band_push_count_kernel(SqWs w) {
-    const int lane = threadIdx.x & 63, i = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const Img m = image(w, blockIdx.y);
-    if (i >= m.eh) return;
-    const bool inner = blockIdx.z != 0;
-    const uint32_t *st = inner ? m.sI : m.sO;
-    uint32_t row = 0;
-    if (i >= 1 && i < m.eh - 1)
-        for (int j0 = 0; j0 < m.ew; j0 += 64 * kBpU) {
-            unsigned c[kBpU];
-            band_push_bits(m.t, st, i, j0, lane, m.ew, c);
-#pragma unroll
-            for (int u = 0; u < kBpU; ++u) {
-                uint32_t tot;
-                (void)wave_scan_small(unsigned(__popc(c[u])), tot);
-                row += tot;
-            }
+    __shared__ BandPushLds L;
+    const Img m = image(w, blockIdx.z);
+    const int i0 = int(blockIdx.y) * kBpTH, j0 = int(blockIdx.x) * kBpTW, c = int(blockIdx.x);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nch = (m.ew + 63) / 64;
+    band_push_tile(m, i0, j0, L);
+    __syncthreads();
+    uint32_t *co = band_push_chunks(m, false), *ci = band_push_chunks(m, true);
+    for (int li = wave; li < kBpTH; li += 4) {
+        const int i = i0 + li;
+        if (i >= m.eh) break;
+        const bool in = i >= 1 && i < m.eh - 1 && j0 + lane < m.ew;
+        uint32_t to, ti;
+        (void)wave_scan_small(in ? unsigned(__popc(band_push_bits(L, li, lane, 1u))) : 0u, to);
+        (void)wave_scan_small(in ? unsigned(__popc(band_push_bits(L, li, lane, 2u))) : 0u, ti);
+        if (lane == 0) {
+            co[int64_t(i) * nch + c] = to;
+            ci[int64_t(i) * nch + c] = ti;
         }
-    if (lane == 0) band_push_rows(m, inner)[i] = row;
+    }
 }
 
 __global__ __launch_bounds__(kThreads) void sq_band_push_scan_kernel(SqWs w) {
     __shared__ uint32_t scr[40];
     const Img m = image(w, blockIdx.x);
     const bool inner = blockIdx.y != 0;
-    uint32_t *rowp = band_push_rows(m, inner);
+    uint32_t *cp = band_push_chunks(m, inner);
+    const int64_t n = int64_t(m.eh) * ((m.ew + 63) / 64);
     uint32_t carry = 0;
-    for (int i0 = 0; i0 < m.eh; i0 += kThreads) {
-        const int i = i0 + threadIdx.x;
-        const uint32_t v = i < m.eh ? rowp[i] : 0u;
+    for (int64_t i0 = 0; i0 < n; i0 += kThreads) {
+        const int64_t i = i0 + threadIdx.x;
+        const uint32_t v = i < n ? cp[i] : 0u;
         uint32_t tot;
         const uint32_t ex = block_scan(v, tot, scr);
-        if (i < m.eh) rowp[i] = carry + ex;
+        if (i < n) cp[i] = carry + ex;
         carry += tot;
     }
     if (threadIdx.x == 0) m.pipe[inner ? kPB0In : kPB0Out] = carry;
 }
 
 __global__ __launch_bounds__(256) void sq_band_push_write_kernel(SqWs w) {
-    const int lane = threadIdx.x & 63, i = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const Img m = image(w, blockIdx.y);
-    if (i < 1 || i >= m.eh - 1) return;
-    const bool inner = blockIdx.z != 0;
-    uint32_t *st = inner ? m.sI : m.sO, *logp = inner ? m.logp : m.olog;
-    const int ew = m.ew;
+    __shared__ BandPushLds L;
+    const Img m = image(w, blockIdx.z);
+    const int i0 = int(blockIdx.y) * kBpTH, j0 = int(blockIdx.x) * kBpTW, c = int(blockIdx.x);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, ew = m.ew, nch = (ew + 63) / 64;
+    band_push_tile(m, i0, j0, L);
+    __syncthreads();  // (every flag the rule reads is in LDS before any stamp store below)
     const int64_t off[4] = {-int64_t(ew), -1, int64_t(ew), 1};
-    // (a chunk's stamp stores cannot change a later chunk's bits: only a
-    // pixel's claimant pushes it, and for its other band neighbours the rule
-    // is false by the band flags alone)
-    uint32_t base = m.meta[0] + band_push_rows(m, inner)[i];
-    for (int j0 = 0; j0 < ew; j0 += 64 * kBpU) {
-        unsigned c[kBpU];
-        band_push_bits(m.t, st, i, j0, lane, ew, c);
+    const uint32_t nb = m.meta[0];
+    for (int li = wave; li < kBpTH; li += 4) {
+        const int i = i0 + li;
+        if (i >= m.eh) break;
+        const bool in = i >= 1 && i < m.eh - 1 && j0 + lane < ew;
+        const int64_t p = int64_t(i) * ew + j0 + lane;
 #pragma unroll
-        for (int u = 0; u < kBpU; ++u) {
+        for (int mk = 0; mk < 2; ++mk) {
+            const bool inner = mk != 0;
+            const unsigned bits = in ? band_push_bits(L, li, lane, inner ? 2u : 1u) : 0u;
             uint32_t tot;
-            uint32_t s = base + wave_scan_small(unsigned(__popc(c[u])), tot);
-            if (c[u]) {
-                const int64_t p = int64_t(i) * ew + j0 + 64 * u + lane;
+            uint32_t s = nb + band_push_chunks(m, inner)[int64_t(i) * nch + c] + wave_scan_small(unsigned(__popc(bits)), tot);
+            uint32_t *st = inner ? m.sI : m.sO, *logp = inner ? m.logp : m.olog;
 #pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    if (c[u] & (1u << q)) {
-                        st[p + off[q]] = s;
-                        logp[s] = uint32_t(p + off[q]);
-                        ++s;
-                    }
-            }
-            base += tot;
+            for (int q = 0; q < 4; ++q)
+                if (bits & (1u << q)) {
+                    st[p + off[q]] = s;
+                    logp[s] = uint32_t(p + off[q]);
+                    ++s;
+                }
         }
     }
 }
@@ -3229,11 +3243,12 @@ int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float 
             hipLaunchKernelGGL(sq_init_kernel, dim3(unsigned((w.eh + 3) / 4), unsigned(nb)), dim3(256), 0, s, w, r);
         hipLaunchKernelGGL(sq_band_scan_kernel, dim3(unsigned(nb)), dim3(kThreads), 0, s, w);
         hipLaunchKernelGGL(sq_band_write_kernel, dim3(unsigned((w.eh + 3) / 4), unsigned(nb)), dim3(256), 0, s, w);
-        hipLaunchKernelGGL(sq_band_push_count_kernel, dim3(unsigned((w.eh + 3) / 4), unsigned(nb), 2u), dim3(256), 0, s,
-                           w);
-        hipLaunchKernelGGL(sq_band_push_scan_kernel, dim3(unsigned(nb), 2u), dim3(kThreads), 0, s, w);
-        hipLaunchKernelGGL(sq_band_push_write_kernel, dim3(unsigned((w.eh + 3) / 4), unsigned(nb), 2u), dim3(256), 0, s,
-                           w);
+        {
+            const dim3 bg(unsigned((w.ew + kBpTW - 1) / kBpTW), unsigned((w.eh + kBpTH - 1) / kBpTH), unsigned(nb));
+            hipLaunchKernelGGL(sq_band_push_count_kernel, bg, dim3(256), 0, s, w);
+            hipLaunchKernelGGL(sq_band_push_scan_kernel, dim3(unsigned(nb), 2u), dim3(kThreads), 0, s, w);
+            hipLaunchKernelGGL(sq_band_push_write_kernel, bg, dim3(256), 0, s, w);
+        }
         const dim3 rgrid(unsigned((w.ew + 63) / 64), unsigned((w.eh + kRecTH - 1) / kRecTH), unsigned(nb));
         // kMW: the shared queues' granules are tagged by slot, which restarts
         // at 0 every fill -- clear the previous fill's tags
