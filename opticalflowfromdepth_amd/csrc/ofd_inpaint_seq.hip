@@ -632,6 +632,171 @@ __global__ __launch_bounds__(256) void sq_band_push_write_kernel(SqWs w) {
     }
 }
 
+// INIT fused with bucket 0's push counts (range + 1 <= kInitR): the tile's
+// hole flags with a halo of max(3, range + 1), so the band is known on the
+// tile with a 2-pixel halo above / left and 1 right, and both marches'
+// INSIDE flags (ring, hole) on the tile with a 1-pixel halo -- the BAND PUSH
+// rule's inputs.  Besides INIT's outputs it stores, per 64-pixel row chunk,
+// the band pixels (the band log's order) and the pushes of each march
+// (sq_band3_scan_kernel, sq_band3_write_kernel take it from there; no row
+// counts, no BAND / COUNT passes).
+static_assert(kInitTW == kBpTW && kInitTH == kBpTH, "INIT and BAND PUSH share their tiles");
+__device__ __forceinline__ uint32_t *band_chunks(const Img &m) { return reinterpret_cast<uint32_t *>(m.k1); }
+
+__global__ __launch_bounds__(256) void sq_init_push_kernel(SqWs w, int range) {
+    constexpr int XW = kInitTW + 2 * kInitR, YH = kInitTH + 2 * kInitR;
+    __shared__ uint8_t hf[YH][XW];               // hole flags, tile + halo h
+    __shared__ uint8_t hor[YH][kInitTW + 2];     // OR over the window's columns, for columns j0 - 1 .. j0 + 64
+    __shared__ BandPushLds P;                    // band / INSIDE flags of the BAND PUSH rule
+    const Img m = image(w, blockIdx.z);
+    const int eh = m.eh, ew = m.ew, r = range, h = max(3, range + 1);
+    const int i0 = int(blockIdx.y) * kInitTH, j0 = int(blockIdx.x) * kInitTW;
+    const int xw = kInitTW + 2 * h, yh = kInitTH + 2 * h;
+    for (int e = threadIdx.x; e < xw * yh; e += 256) {
+        const int ry = e / xw, rx = e - ry * xw;
+        const int y = i0 - h + ry, x = j0 - h + rx;
+        hf[ry][rx] = (y > 0 && x > 0 && y < eh - 1 && x < ew - 1 && m.sI[int64_t(y) * ew + x] == INF) ? 1 : 0;
+    }
+    __syncthreads();
+    // hor[ry][k]: a hole in columns (j0 - 1 + k) - r .. + r of halo row ry
+    for (int e = threadIdx.x; e < yh * (kInitTW + 2); e += 256) {
+        const int ry = e / (kInitTW + 2), k = e - ry * (kInitTW + 2);
+        uint8_t o = 0;
+        for (int d = 0; d <= 2 * r; ++d) o |= hf[ry][k + h - 1 - r + d];
+        hor[ry][k] = o;
+    }
+    auto hole = [&](int y, int x) -> bool { return hf[y - i0 + h][x - j0 + h] != 0; };  // |y - i0|, |x - j0| in the halo
+    auto bandp = [&](int y, int x) -> bool {
+        return y > 0 && x > 0 && y < eh - 1 && x < ew - 1 && !hole(y, x) &&
+               (hole(y - 1, x) || hole(y + 1, x) || hole(y, x - 1) || hole(y, x + 1));
+    };
+    for (int e = threadIdx.x; e < (kBpTH + 2) * (kBpTW + 3); e += 256) {
+        const int rr = e / (kBpTW + 3), c = e - rr * (kBpTW + 3);
+        P.band[rr][c] = bandp(i0 - 2 + rr, j0 - 2 + c) ? 1 : 0;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < (kBpTH + 2) * (kBpTW + 2); e += 256) {
+        const int rr = e / (kBpTW + 2), c = e - rr * (kBpTW + 2);
+        const int y = i0 - 1 + rr, x = j0 - 1 + c;
+        bool ring = false;
+        const bool hl = y > 0 && x > 0 && y < eh - 1 && x < ew - 1 && hole(y, x);
+        if (y > 0 && x > 0 && y < eh - 1 && x < ew - 1 && !hl && !bandp(y, x))  // (row i0 + 16 is past P.band)
+            for (int d = 0; d <= 2 * r && !ring; ++d) ring = hor[rr + h - 1 - r + d][c] != 0;
+        P.ins[rr][c] = uint8_t((ring ? 1 : 0) | (hl ? 2 : 0));
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, j = j0 + lane, c = int(blockIdx.x);
+    const int nch = (ew + 63) / 64;
+    uint32_t *cb = band_chunks(m), *co = band_push_chunks(m, false), *ci = band_push_chunks(m, true);
+    for (int li = wave; li < kInitTH; li += 4) {
+        const int i = i0 + li;
+        if (i >= eh) break;  // wave-uniform
+        bool band = false;
+        unsigned po = 0, pi = 0;
+        if (j < ew) {
+            const int64_t p = int64_t(i) * ew + j;
+            const bool frame = i == 0 || j == 0 || i == eh - 1 || j == ew - 1;
+            band = P.band[li + 2][lane + 2] != 0;
+            if (frame) m.sI[p] = 0u;
+            m.sO[p] = (P.ins[li + 1][lane + 1] & 1u) ? INF : 0u;
+            m.t[p] = band ? 0.f : T_FAR;
+            m.own[p] = INF;
+            m.kc[p] = 0u;
+            po = band_push_bits(P, li, lane, 1u);
+            pi = band_push_bits(P, li, lane, 2u);
+        }
+        uint32_t tb, to, ti;
+        (void)wave_scan_small(band ? 1u : 0u, tb);
+        (void)wave_scan_small(unsigned(__popc(po)), to);
+        (void)wave_scan_small(unsigned(__popc(pi)), ti);
+        if (lane == 0) {
+            cb[int64_t(i) * nch + c] = tb;
+            co[int64_t(i) * nch + c] = to;
+            ci[int64_t(i) * nch + c] = ti;
+        }
+    }
+}
+
+// Offsets of the three per-chunk counts (band, outer pushes, inner pushes) in
+// raster order, one workgroup per image; also the per-fill meta / pipe reset
+// (sq_band_scan_kernel's) with the band's size in meta[0].
+__global__ __launch_bounds__(kThreads) void sq_band3_scan_kernel(SqWs w) {
+    __shared__ uint32_t scr[40];
+    const Img m = image(w, blockIdx.x);
+    const int64_t n = int64_t(m.eh) * ((m.ew + 63) / 64);
+    uint32_t tot3[3];
+    for (int a = 0; a < 3; ++a) {
+        uint32_t *cp = a == 0 ? band_chunks(m) : band_push_chunks(m, a == 2);
+        uint32_t carry = 0;
+        for (int64_t i0 = 0; i0 < n; i0 += kThreads) {
+            const int64_t i = i0 + threadIdx.x;
+            const uint32_t v = i < n ? cp[i] : 0u;
+            uint32_t tot;
+            const uint32_t ex = block_scan(v, tot, scr);
+            if (i < n) cp[i] = carry + ex;
+            carry += tot;
+        }
+        tot3[a] = carry;
+    }
+    if (threadIdx.x == 0) {
+        for (int k = 0; k < kMeta; ++k) m.meta[k] = 0u;
+        for (int k = 0; k < kPipe; ++k) m.pipe[k] = 0u;
+        m.meta[0] = tot3[0];
+        m.pipe[kPB0Out] = tot3[1];
+        m.pipe[kPB0In] = tot3[2];
+    }
+}
+
+// The band log (raster order, T = 0, both marches' logs) and bucket 0's
+// pushes, on INIT's tiles: the rule's flags come from INIT's outputs (band:
+// distance 0; INSIDE: stamp INF), read before any stamp store of this
+// workgroup (only a pixel's claimant pushes it: another workgroup's stores
+// cannot change a bit this one computes).
+__global__ __launch_bounds__(256) void sq_band3_write_kernel(SqWs w) {
+    __shared__ BandPushLds L;
+    const Img m = image(w, blockIdx.z);
+    const int i0 = int(blockIdx.y) * kBpTH, j0 = int(blockIdx.x) * kBpTW, c = int(blockIdx.x);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, ew = m.ew, nch = (ew + 63) / 64;
+    band_push_tile(m, i0, j0, L);
+    __syncthreads();
+    const int64_t off[4] = {-int64_t(ew), -1, int64_t(ew), 1};
+    const uint32_t nb = m.meta[0];
+    float *ologt = reinterpret_cast<float *>(m.olog + m.en);
+    for (int li = wave; li < kBpTH; li += 4) {
+        const int i = i0 + li;
+        if (i >= m.eh) break;
+        const bool in = i >= 1 && i < m.eh - 1 && j0 + lane < ew;
+        const int64_t p = int64_t(i) * ew + j0 + lane;
+        const int64_t ck = int64_t(i) * nch + c;
+        {
+            const bool band = in && L.band[li + 2][lane + 2];
+            uint32_t tot;
+            const uint32_t s = band_chunks(m)[ck] + wave_scan_small(band ? 1u : 0u, tot);
+            if (band) {
+                m.logp[s] = uint32_t(p);
+                m.logt[s] = 0.f;
+                m.olog[s] = uint32_t(p);
+                ologt[s] = 0.f;
+            }
+        }
+#pragma unroll
+        for (int mk = 0; mk < 2; ++mk) {
+            const bool inner = mk != 0;
+            const unsigned bits = in ? band_push_bits(L, li, lane, inner ? 2u : 1u) : 0u;
+            uint32_t tot;
+            uint32_t s = nb + band_push_chunks(m, inner)[ck] + wave_scan_small(unsigned(__popc(bits)), tot);
+            uint32_t *st = inner ? m.sI : m.sO, *logp = inner ? m.logp : m.olog;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (bits & (1u << q)) {
+                    st[p + off[q]] = s;
+                    logp[s] = uint32_t(p + off[q]);
+                    ++s;
+                }
+        }
+    }
+}
+
 // ---------------------------------------------------------------- FMM
 constexpr int kHash = 1024;  // distinct-distance sort of large buckets: hash slots
 constexpr int kMaxD = 256;   // ... and distinct distances it handles (else the merge sort)
@@ -3234,17 +3399,21 @@ int ofd_inpaint_telea_seq_f32(const float *img, const float *valid, const float 
     auto run_chunk = [&](const SqWs &w, int64_t b0, int64_t nb, hipStream_t s) {
         hipLaunchKernelGGL(sq_prep_tile_kernel, dim3(unsigned((W + 63) / 64), unsigned((H + 15) / 16), unsigned(nb)),
                            dim3(256), 0, s, img, valid, collision, out, w, int(C), int(H), int(W), b0, rec3 ? 1 : 0);
-        if (r <= kInitR)
-            hipLaunchKernelGGL(sq_init_tile_kernel,
-                               dim3(unsigned((w.ew + kInitTW - 1) / kInitTW), unsigned((w.eh + kInitTH - 1) / kInitTH),
-                                    unsigned(nb)),
-                               dim3(256), 0, s, w, r);
-        else
-            hipLaunchKernelGGL(sq_init_kernel, dim3(unsigned((w.eh + 3) / 4), unsigned(nb)), dim3(256), 0, s, w, r);
-        hipLaunchKernelGGL(sq_band_scan_kernel, dim3(unsigned(nb)), dim3(kThreads), 0, s, w);
-        hipLaunchKernelGGL(sq_band_write_kernel, dim3(unsigned((w.eh + 3) / 4), unsigned(nb)), dim3(256), 0, s, w);
-        {
-            const dim3 bg(unsigned((w.ew + kBpTW - 1) / kBpTW), unsigned((w.eh + kBpTH - 1) / kBpTH), unsigned(nb));
+        const dim3 bg(unsigned((w.ew + kBpTW - 1) / kBpTW), unsigned((w.eh + kBpTH - 1) / kBpTH), unsigned(nb));
+        if (r + 1 <= kInitR) {  // INIT with bucket 0's push counts, one scan, the band log and pushes
+            hipLaunchKernelGGL(sq_init_push_kernel, bg, dim3(256), 0, s, w, r);
+            hipLaunchKernelGGL(sq_band3_scan_kernel, dim3(unsigned(nb)), dim3(kThreads), 0, s, w);
+            hipLaunchKernelGGL(sq_band3_write_kernel, bg, dim3(256), 0, s, w);
+        } else {
+            if (r <= kInitR)
+                hipLaunchKernelGGL(sq_init_tile_kernel,
+                                   dim3(unsigned((w.ew + kInitTW - 1) / kInitTW), unsigned((w.eh + kInitTH - 1) / kInitTH),
+                                        unsigned(nb)),
+                                   dim3(256), 0, s, w, r);
+            else
+                hipLaunchKernelGGL(sq_init_kernel, dim3(unsigned((w.eh + 3) / 4), unsigned(nb)), dim3(256), 0, s, w, r);
+            hipLaunchKernelGGL(sq_band_scan_kernel, dim3(unsigned(nb)), dim3(kThreads), 0, s, w);
+            hipLaunchKernelGGL(sq_band_write_kernel, dim3(unsigned((w.eh + 3) / 4), unsigned(nb)), dim3(256), 0, s, w);
             hipLaunchKernelGGL(sq_band_push_count_kernel, bg, dim3(256), 0, s, w);
             hipLaunchKernelGGL(sq_band_push_scan_kernel, dim3(unsigned(nb), 2u), dim3(kThreads), 0, s, w);
             hipLaunchKernelGGL(sq_band_push_write_kernel, bg, dim3(256), 0, s, w);
