@@ -2494,6 +2494,9 @@ constexpr int kPGh = 54, kPGt = 55, kPGo = 56;
 #define OFD_MW_THR 512
 #endif
 static_assert(OFD_MW_THR <= 512, "kMW overflow slices are sized for at most 8 waves per workgroup");
+#ifndef OFD_MW_APPEND_WAIT  // kMW: 1 = every append waits for its count to land (A/B)
+#define OFD_MW_APPEND_WAIT 0
+#endif
 #ifndef OFD_MW_RELOAD  // kMW: a waiting hole re-reads a missing neighbour's word every this many tries
 #define OFD_MW_RELOAD 2
 #endif
@@ -2888,14 +2891,23 @@ __global__ __launch_bounds__(kThr) void sq_colour3df_kernel(SqWs w, int C, int H
                 if (lane == 63) {
                     hq = __hip_atomic_load(&L.qh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     if constexpr (kMW) {
-                        // counted before any of them can be taken (the add has
-                        // returned before the slots are published), so the
-                        // image's count never misses a queued hole
+                        // Holes for the shared queue are counted before any of
+                        // them can be taken (the add has returned before the
+                        // slots are published), so the image's count never
+                        // misses a hole another workgroup could take.  Holes
+                        // for this workgroup's LDS queue are held by it (it
+                        // does not leave while its queue or a batch holds any),
+                        // so their add need not land first: a count read too
+                        // early can only make another workgroup leave sooner.
                         const uint32_t len = __hip_atomic_load(&L.qr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) - hq;
                         sp = len + tot > uint32_t(OFD_MW_CAP) ? 1u : 0u;
                         (void)__hip_atomic_fetch_add(pw + kPGo, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         rb = sp ? atomicAdd(pw + kPGt, tot) : atomicAdd(&L.qr, tot);
+#if OFD_MW_APPEND_WAIT
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#else
+                        if (sp) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
                     } else {
                         rb = atomicAdd(&L.qr, tot);
                     }
@@ -3102,6 +3114,12 @@ __global__ __launch_bounds__(kThr) void sq_colour3df_kernel(SqWs w, int C, int H
         if (tid == 0 && wr == 0 && pq <= hq &&
             __hip_atomic_load(pw + kPGo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
             put64(m.pipe + kPTc1, wall_clock64());
+#ifdef OFD_SQ_PROF
+        if (tid == 0 && wr == 0) {  // wave 0 of the image's first workgroup, all rounds
+            for (int k = 0; k < 8; ++k) m.meta[16 + k] += uint32_t(prof[k] >> 8);
+            m.meta[7] += batches;
+        }
+#endif
         return;
     }
     // the unclaimed entries still in the ring go to fr2 for the next round

@@ -87,7 +87,7 @@ def main():
     pi_ = a256(en * 4) * 6 + a256(en * 8) * 2 + a256(eh * 4) + 32 * 4 + en * 160 + 768 * 1024 * 4 + en * 8 + 768
     G = min(B, (ws.numel() - 2048) // pi_)
     k1 = 6 * a256(G * en * 4) + a256(G * en * 8)
-    kdeep = int(np.argmax(m[:, 3]))
+    kdeep = int(np.argmax(m[:, 3])) if m[:, 3].any() else int(np.argmax(m[:, 7]))  # levels-free pass: most batches
     L = int(m[kdeep, 3])
     if not os.environ.get("OFD_SEQ_COLOUR", "").startswith("g"):  # level sizes: the g16 colour kernel only
         print(f"deepest image {kdeep}: {L} levels")
