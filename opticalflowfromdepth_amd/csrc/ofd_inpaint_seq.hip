@@ -2782,24 +2782,30 @@ __global__ __launch_bounds__(kThr) void sq_colour3df_kernel(SqWs w, int C, int H
                     const bool reload = kMW ? (tries % OFD_MW_RELOAD) == OFD_MW_RELOAD - 1 : (tries & 7) == 7;
 #pragma unroll
                     for (int k = 0; k < 8; ++k) asm volatile("" : "+v"(tb[k]));  // no hoisted offsets (spills)
+                    // every pending cell's lookup first (the table, else on a
+                    // reload try the word itself: all reloads in flight at
+                    // once), then the flags
+                    uint32_t wvk[8];
 #pragma unroll
-                    for (int k = 0; k < 8; ++k)
+                    for (int k = 0; k < 8; ++k) {
+                        wvk[k] = 0u;
                         if (pend & (1u << k)) {
                             const uint32_t q = p + uint32_t(WOFF(k));
                             const uint64_t ce = __hip_atomic_load(&L.ct[q & uint32_t(kDfCt - 1)], __ATOMIC_RELAXED,
                                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-                            uint32_t wv = uint32_t(ce >> 32);
-                            if (uint32_t(ce) != q + 1u) {
-                                wv = 0u;
-                                if (reload)  // an interior hole: no clamp
-                                    wv = __hip_atomic_load(
-                                        m.shd + IX32((i - 5 + WC(k) / 9) * W + (j - 5 + WC(k) % 9)), __ATOMIC_RELAXED,
-                                        __HIP_MEMORY_SCOPE_AGENT);
-                            }
-                            if ((wv >> 24) != 0u) {
-                                gv[WC(k)] = wv;
-                                pend &= ~(1u << k);
-                            }
+                            if (uint32_t(ce) == q + 1u)
+                                wvk[k] = uint32_t(ce >> 32);
+                            else if (reload)  // an interior hole: no clamp
+                                wvk[k] = __hip_atomic_load(
+                                    m.shd + IX32((i - 5 + WC(k) / 9) * W + (j - 5 + WC(k) % 9)), __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);
+                        }
+                    }
+#pragma unroll
+                    for (int k = 0; k < 8; ++k)
+                        if ((pend & (1u << k)) && (wvk[k] >> 24) != 0u) {
+                            gv[WC(k)] = wvk[k];
+                            pend &= ~(1u << k);
                         }
                     if (!__any(pend != 0u)) break;
                     __builtin_amdgcn_s_sleep(OFD_DF_SLEEP);
@@ -2879,13 +2885,18 @@ __global__ __launch_bounds__(kThr) void sq_colour3df_kernel(SqWs w, int C, int H
                 for (int k = 0; k < 8; ++k) rmask |= (old[k] + 1u == kK ? 1u : 0u) << k;
                 const uint32_t cnt = uint32_t(__popc(rmask));
                 const int lane = tid & 63;
-                uint32_t incl = cnt;
+                // inclusive prefix of cnt (0..8) over the wave by bit planes:
+                // four ballots instead of six dependent lane shuffles
+                uint32_t incl = 0, tot = 0;
+                {
+                    const uint64_t upto = ~uint64_t(0) >> (63 - lane);
 #pragma unroll
-                for (int d = 1; d < 64; d <<= 1) {
-                    const uint32_t y = __shfl_up(incl, d);
-                    if (lane >= d) incl += y;
+                    for (int k = 0; k < 4; ++k) {
+                        const uint64_t bal = __ballot((cnt >> k) & 1u);
+                        incl += uint32_t(__popcll(bal & upto)) << k;
+                        tot += uint32_t(__popcll(bal)) << k;
+                    }
                 }
-                const uint32_t tot = __shfl(incl, 63);
                 if (tot == 0u) return;  // wave-uniform
                 uint32_t rb = 0, hq = 0, sp = 0;
                 if (lane == 63) {
